@@ -1,0 +1,132 @@
+/*
+ * layout.h — the flattened scene as it lives in HBM (one blob per device, uploaded once at commit).
+ *
+ * The reference scene is an object graph of Box<dyn Hittable> (src/hittable/).  It is lowered into
+ *   nodes  : the world tree in DFS PRE-ORDER, 32 B per node (two 16-B loads).  A box node stores its
+ *            `skip` = index one past its subtree, so the reference's recursive BvhNode::hit
+ *            (bvh_node.rs:104-127: left subtree, then right subtree with the shrunken t_max) is a
+ *            stackless loop: box passes -> i+1, box fails -> skip.  Lists/Cuboids are consecutive
+ *            PRIM nodes (list.rs:20-31 order), Translation/Rotation are BEGIN/END brackets that
+ *            transform / restore the ray, a ConstantMedium is one MEDIUM node whose boundary subtree
+ *            is emitted after the main stream ([bstart, bend)).
+ *   prims  : sphere / moving sphere / rect records, 48 B.
+ *   insts, media, mats, texs, perlin tables, image bytes.
+ * Every section is 256-B aligned inside the blob.
+ */
+#pragma once
+#include <stdint.h>
+
+namespace hrt {
+namespace gpu {
+
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr int MAX_INST_DEPTH = 8;
+
+/* node kinds (Node.kp >> 24) */
+enum : uint32_t {
+  K_BOX = 0,        /* BvhNode box: pass -> i+1, fail -> skip */
+  K_BOX_PRIM = 1,   /* BvhNode leaf holding one primitive: box, then prim[payload] */
+  K_PRIM = 2,       /* primitive without box (List / Cuboid side / root) */
+  K_INST_BEGIN = 3, /* Translation / Rotation: transform ray (payload = inst) */
+  K_INST_END = 4,   /* restore ray */
+  K_MEDIUM = 5      /* ConstantMedium (payload = medium) */
+};
+struct alignas(16) Node {
+  float mn[3];
+  uint32_t skip;
+  float mx[3];
+  uint32_t kp; /* kind << 24 | payload */
+};
+static_assert(sizeof(Node) == 32, "node is two dwordx4");
+
+enum : uint32_t { P_SPHERE = 0, P_MOVING = 1, P_RECT = 2 };
+/* sphere : p0 = (cx, cy, cz, r)
+ * moving : p0 = (c0, r), p1 = (c1 - c0, time_start), p2[0] = time_end - time_start
+ *          (both differences are exactly what moving_sphere.rs:55-58 computes per call)
+ * rect   : p0 = (a0, a1, b0, b1), p1 = (k, a1 - a0, b1 - b0, 0)
+ * km     = kind | plane << 2 | material << 4 */
+struct alignas(16) Prim {
+  float p0[4];
+  float p1[4];
+  float p2[2];
+  uint32_t parent; /* enclosing instance (NONE at world level) */
+  uint32_t km;
+};
+static_assert(sizeof(Prim) == 48, "prim is three dwordx4");
+
+enum : uint32_t { I_TRANSLATE = 0, I_ROTATE = 1 };
+struct alignas(16) Inst {
+  float d[3];     /* translation displacement */
+  float sin_t;    /* rotation */
+  float cos_t;
+  uint32_t axis;  /* HRT_AXIS_* */
+  uint32_t parent;
+  uint32_t kind;
+};
+
+struct alignas(16) Medium {
+  float neg_inv_density;
+  uint32_t bstart, bend;
+  uint32_t mat; /* Isotropic phase function */
+  uint32_t medium_id;
+  uint32_t parent;
+  uint32_t pad0, pad1;
+};
+
+enum : uint32_t { M_LAMBERTIAN = 0, M_METAL = 1, M_DIELECTRIC = 2, M_DIFFUSE_LIGHT = 3, M_ISOTROPIC = 4 };
+/* lambertian/diffuse_light/isotropic: tex; metal: a = (albedo, fuzz); dielectric: a[0] = ior */
+struct alignas(16) Mat {
+  float a[4];
+  uint32_t kind, tex;
+  uint32_t needs_uv; /* texture tree reads (u, v) (only ImageTexture does) */
+  uint32_t pad;
+};
+
+enum : uint32_t { T_SOLID = 0, T_CHECKER = 1, T_NOISE = 2, T_IMAGE = 3 };
+/* solid: a = color; checker: i0 odd, i1 even; noise: a[0] scale, i0 perlin table;
+ * image: i0 byte offset, i1 width, i2 height, i3 components (width == 0 -> magenta) */
+struct alignas(16) Tex {
+  float a[4];
+  uint32_t kind, i0, i1, i2;
+  uint32_t i3, pad0, pad1, pad2;
+};
+
+struct alignas(16) Perlin {
+  float ranvec[256][4];
+  uint32_t perm[3][256];
+};
+
+/* tile list entry (device) */
+struct alignas(16) TileDev {
+  uint32_t x, y, w, h;
+  uint32_t bw;        /* ceil(w / 8) */
+  uint32_t pad_start; /* first padded work index of this tile */
+  uint32_t out_off;   /* first output pixel of this tile */
+  uint32_t pad;
+};
+
+/* feature bits (scene-wide) */
+enum : uint32_t {
+  F_MOVING = 1u << 0,
+  F_RECT = 1u << 1,
+  F_INSTANCE = 1u << 2,
+  F_MEDIUM = 1u << 3,
+  F_NOISE = 1u << 4,
+  F_IMAGE = 1u << 5,
+  F_CHECKER = 1u << 6,
+  F_LIGHT = 1u << 7,
+  F_ISOTROPIC = 1u << 8,
+  F_METAL = 1u << 9,
+  F_DIELECTRIC = 1u << 10
+};
+/* what the lean kernel instantiation handles (the BASELINE headline scene needs only these) */
+constexpr uint32_t F_BASIC = F_MOVING | F_CHECKER | F_METAL | F_DIELECTRIC;
+
+/* box-culling modes */
+enum : int {
+  CULL_REFERENCE = 0, /* aabb.rs:20-47 verbatim: each axis tested alone against [t_min, t_max] */
+  CULL_SLAB = 1       /* intervals narrowed across axes (a subset of the reference's passes) */
+};
+
+}  // namespace gpu
+}  // namespace hrt

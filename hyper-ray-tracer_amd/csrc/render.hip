@@ -1,0 +1,889 @@
+/*
+ * render.hip — the gfx950 path-tracing megakernel and its device runtime (scene upload, launches).
+ *
+ * Replaces the per-tile task body of Application::render (src/application.rs:415-473) and
+ * ray_color (:477-495) of SkillerRaptor/hyper-ray-tracer, including everything they reach through
+ * dyn Hittable / Material / Texture.  One persistent launch renders a whole tile set:
+ *
+ *   - each LANE owns one pixel at a time and runs its spp samples back to back (the reference's
+ *     sample loop, :443-449, so the per-pixel sum keeps the reference's order); when its pixel is
+ *     done it takes the next one from a global work counter, claimed once per wave with a ballot +
+ *     one atomicAdd (no lane idles while work remains);
+ *   - every iteration of the wave loop advances every busy lane by exactly one ray segment
+ *     (= one world.hit call): lanes whose path ended start their next sample in the same iteration;
+ *   - the world is the pre-order node stream of layout.h, walked stackless with skip links in the
+ *     reference's left-then-right order with the shrinking t_max, so closest hits, tie-breaks and
+ *     medium evaluation agree with the recursive BvhNode::hit;
+ *   - the hit record (point/normal/uv/front_face) is built once per segment for the winning
+ *     primitive only, replaying the enclosing Translation/Rotation chain exactly as the reference
+ *     recursion does; (u, v) are evaluated only when the material's texture reads them;
+ *   - randomness: per-(pixel, sample) xoshiro128** streams (hd_math.h) drawn in the reference's
+ *     order; ConstantMedium draws come from a (path, segment, medium) keyed sub-stream.
+ * No MFMA: this is branchy 3-vector math.  All arithmetic on the branch-deciding path is shared with
+ * the CPU oracle through hd_math.h and compiled with -ffp-contract=off.
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "scene_internal.h"
+
+using namespace hrt;
+namespace G = hrt::gpu;
+
+namespace {
+
+/* ------------------------------------------------------------------ kernel parameters */
+struct KParams {
+  const G::Node* nodes;
+  const G::Prim* prims;
+  const G::Inst* insts;
+  const G::Medium* media;
+  const G::Mat* mats;
+  const G::Tex* texs;
+  const G::Perlin* perlin;
+  const uint8_t* images;
+  uint32_t main_end;
+  float ln_e;
+  /* camera (camera.rs:16-31 after resize) */
+  Vec3 cam_origin, cam_llc, cam_h, cam_v, cam_u, cam_vv;
+  float lens_radius, time0, time1;
+  /* render */
+  uint32_t W, H, spp, max_depth, sample_offset;
+  float t_min;
+  Vec3 background;
+  uint64_t seed;
+  /* work */
+  const G::TileDev* tiles;
+  uint32_t n_tiles;
+  uint32_t total_work;
+  float4* out;
+  uint32_t* counter;
+  unsigned long long* stats; /* segments, samples, pixels */
+};
+
+struct TRay {
+  Vec3 o, d, inv;
+  float time;
+  float dd; /* dot(d, d): sphere.rs:42 `a`, constant for the ray */
+};
+
+__device__ __forceinline__ void set_ray(TRay& r, Vec3 o, Vec3 d, float time) {
+  r.o = o;
+  r.d = d;
+  r.time = time;
+  /* aabb.rs:22 computes 1/d per call; the value is the same every time */
+  r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  r.dd = dot(d, d);
+}
+
+__device__ __forceinline__ float4 ld4(const void* p) { return *reinterpret_cast<const float4*>(p); }
+
+/* aabb.rs:20-47 (CULL_REFERENCE) or its narrowed form (CULL_SLAB) */
+template <int CULL>
+__device__ __forceinline__ bool box_hit(const float4& a, const float4& b, const TRay& r, float tmin,
+                                        float tmax) {
+  const float mn[3] = {a.x, a.y, a.z}, mx[3] = {b.x, b.y, b.z};
+  const float o[3] = {r.o.x, r.o.y, r.o.z}, inv[3] = {r.inv.x, r.inv.y, r.inv.z};
+  if (CULL == G::CULL_REFERENCE) {
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      float ts = (mn[k] - o[k]) * inv[k];
+      float te = (mx[k] - o[k]) * inv[k];
+      if (inv[k] < 0.0f) { float t = ts; ts = te; te = t; }
+      float lo = ts > tmin ? ts : tmin;
+      float hi = te < tmax ? te : tmax;
+      ok = ok & !(hi <= lo);
+    }
+    return ok;
+  } else {
+    float lo = tmin, hi = tmax;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      float ts = (mn[k] - o[k]) * inv[k];
+      float te = (mx[k] - o[k]) * inv[k];
+      if (inv[k] < 0.0f) { float t = ts; ts = te; te = t; }
+      lo = ts > lo ? ts : lo;
+      hi = te < hi ? te : hi;
+    }
+    return !(hi <= lo);
+  }
+}
+
+/* sphere.rs:38-55 / moving_sphere.rs:61-78: the accepted root only */
+__device__ __forceinline__ bool sphere_root(const G::Prim* pp, uint32_t kind, const TRay& r, float tmin,
+                                            float tmax, float& root) {
+  float4 p0 = ld4(pp->p0);
+  Vec3 c = v3(p0.x, p0.y, p0.z);
+  if (kind == G::P_MOVING) {
+    float4 p1 = ld4(pp->p1);
+    float span = pp->p2[0];
+    c = c + ((r.time - p1.w) / span) * v3(p1.x, p1.y, p1.z);
+  }
+  Vec3 oc = r.o - c;
+  float a = r.dd;
+  float half_b = dot(oc, r.d);
+  float cc = dot(oc, oc) - p0.w * p0.w;
+  float disc = half_b * half_b - a * cc;
+  if (disc < 0.0f) return false;
+  float sq = sqrtf(disc);
+  float t = (-half_b - sq) / a;
+  if (t < tmin || tmax < t) {
+    t = (-half_b + sq) / a;
+    if (t < tmin || tmax < t) return false;
+  }
+  root = t;
+  return true;
+}
+
+__device__ __forceinline__ void plane_axes(uint32_t plane, int& k, int& a, int& b) {
+  /* rect.rs:55-59 */
+  if (plane == HRT_PLANE_XY) { k = 2; a = 0; b = 1; }
+  else if (plane == HRT_PLANE_YZ) { k = 0; a = 1; b = 2; }
+  else { k = 1; a = 2; b = 0; }
+}
+
+/* rect.rs:53-68 */
+__device__ __forceinline__ bool rect_t(const G::Prim* pp, uint32_t plane, const TRay& r, float tmin,
+                                       float tmax, float& tout) {
+  int k, a, b;
+  plane_axes(plane, k, a, b);
+  float4 p0 = ld4(pp->p0);
+  float kk = pp->p1[0];
+  float t = (kk - r.o[k]) / r.d[k];
+  if (t < tmin || t > tmax) return false;
+  float av = r.o[a] + t * r.d[a];
+  float bv = r.o[b] + t * r.d[b];
+  if (av < p0.x || av > p0.y || bv < p0.z || bv > p0.w) return false;
+  tout = t;
+  return true;
+}
+
+/* translation.rs:26-30 and rotation.rs:104-117: the ray handed to the child */
+__device__ __forceinline__ void inst_ray(const G::Inst& in, Vec3& o, Vec3& d) {
+  if (in.kind == G::I_TRANSLATE) {
+    o = o - v3(in.d[0], in.d[1], in.d[2]);
+    return;
+  }
+  int a = (int)(in.axis + 1) % 3, b = (int)(in.axis + 2) % 3;
+  float s = in.sin_t, c = in.cos_t;
+  Vec3 no = o, nd = d;
+  no[a] = c * o[a] + s * o[b];
+  no[b] = -s * o[a] + c * o[b];
+  nd[a] = c * d[a] + s * d[b];
+  nd[b] = -s * d[a] + c * d[b];
+  o = no;
+  d = nd;
+}
+
+struct PathKey {
+  uint64_t pkey;
+  uint32_t segment;
+};
+
+/* The world walk.  Closest hit over [begin, end) of the node stream with t in [tmin, closest]:
+ * `winner` = node index of the accepted leaf (NONE if nothing).  MEDIA: ConstantMedium nodes are
+ * evaluated (their boundary walks are nested calls with MEDIA = false). */
+template <int CULL, bool FULL, bool MEDIA>
+__device__ void trace(const KParams& P, uint32_t begin, uint32_t end, Vec3 o, Vec3 d, float time,
+                      float tmin, float& closest, uint32_t& winner, const PathKey& pk) {
+  TRay r;
+  set_ray(r, o, d, time);
+  Vec3 so[G::MAX_INST_DEPTH], sd[G::MAX_INST_DEPTH];
+  int sp = 0;
+  uint32_t i = begin;
+  while (i < end) {
+    const G::Node* np = P.nodes + i;
+    const float4 a = ld4(np->mn);
+    const float4 b = ld4(np->mx);
+    const uint32_t kp = __float_as_uint(b.w);
+    const uint32_t kind = kp >> 24;
+    const uint32_t payload = kp & 0xFFFFFFu;
+    const uint32_t here = i;
+    if (kind <= G::K_BOX_PRIM) {
+      bool pass = box_hit<CULL>(a, b, r, tmin, closest);
+      if (kind == G::K_BOX) {
+        i = pass ? i + 1 : __float_as_uint(a.w);
+        continue;
+      }
+      i++;
+      if (!pass) continue;
+    } else if (kind == G::K_PRIM) {
+      i++;
+    } else {
+      if constexpr (FULL) {
+        i++;
+        if (kind == G::K_INST_BEGIN) {
+          so[sp] = r.o;
+          sd[sp] = r.d;
+          sp++;
+          Vec3 no = r.o, nd = r.d;
+          inst_ray(P.insts[payload], no, nd);
+          set_ray(r, no, nd, r.time);
+        } else if (kind == G::K_INST_END) {
+          sp--;
+          set_ray(r, so[sp], sd[sp], r.time);
+        } else if (kind == G::K_MEDIUM) {
+          if constexpr (MEDIA) {
+            /* constant_medium.rs:34-76 */
+            const G::Medium m = P.media[payload];
+            const float inf = __uint_as_float(0x7f800000u);
+            float c1 = inf, c2 = inf;
+            uint32_t w1 = G::NONE, w2 = G::NONE;
+            trace<CULL, FULL, false>(P, m.bstart, m.bend, r.o, r.d, r.time, -inf, c1, w1, pk);
+            if (w1 == G::NONE) continue;
+            trace<CULL, FULL, false>(P, m.bstart, m.bend, r.o, r.d, r.time, c1 + 0.0001f, c2, w2, pk);
+            if (w2 == G::NONE) continue;
+            float r1 = c1, r2 = c2;
+            if (r1 < tmin) r1 = tmin;
+            if (r2 > closest) r2 = closest;
+            if (r1 >= r2) continue;
+            if (r1 < 0.0f) r1 = 0.0f;
+            float ray_length = sqrtf(r.dd);
+            float inside = (r2 - r1) * ray_length;
+            float xi = medium_xi(pk.pkey, pk.segment, m.medium_id);
+            float hit_distance = m.neg_inv_density * (ln_f(xi) / P.ln_e);
+            if (hit_distance > inside) continue;
+            closest = r1 + hit_distance / ray_length;
+            winner = here;
+          }
+        }
+      }
+      continue;
+    }
+    /* one primitive (payload) */
+    const G::Prim* pp = P.prims + payload;
+    const uint32_t km = pp->km;
+    const uint32_t pkind = km & 3u;
+    float t;
+    bool h;
+    if (FULL && pkind == G::P_RECT) h = rect_t(pp, (km >> 2) & 3u, r, tmin, closest, t);
+    else h = sphere_root(pp, pkind, r, tmin, closest, t);
+    if (h) {
+      closest = t;
+      winner = here;
+    }
+  }
+}
+
+/* ------------------------------------------------------------------ hit record + shading */
+struct Rec {
+  Vec3 p, n;
+  float u, v;
+  bool front;
+  uint32_t mat;
+};
+
+__device__ __forceinline__ void set_face_normal(Rec& rec, Vec3 dir, Vec3 outward) {
+  rec.front = dot(dir, outward) < 0.0f;
+  rec.n = rec.front ? outward : -outward;
+}
+
+/* sphere.rs:31-35 */
+__device__ __forceinline__ void sphere_uv(Vec3 p, float& u, float& v) {
+  float theta = acos_f(-p.y);
+  float phi = atan2_f(-p.z, p.x) + PI_F;
+  u = phi / (2.0f * PI_F);
+  v = theta / PI_F;
+}
+
+/* Record of the winning leaf in world space (hit_record.rs, sphere.rs:57-73, rect.rs:70-83,
+ * constant_medium.rs:66-75, then translation.rs:33-35 / rotation.rs:119-132 on the way out). */
+template <bool FULL>
+__device__ Rec make_record(const KParams& P, uint32_t winner, float t, Vec3 wo, Vec3 wd, float time) {
+  const G::Node* np = P.nodes + winner;
+  const uint32_t kp = np->kp;
+  const uint32_t kind = kp >> 24, payload = kp & 0xFFFFFFu;
+  Rec rec;
+  rec.u = 0.0f;
+  rec.v = 0.0f;
+  if constexpr (!FULL) {
+    const G::Prim* pp = P.prims + payload;
+    const uint32_t km = pp->km;
+    float4 p0 = ld4(pp->p0);
+    Vec3 c = v3(p0.x, p0.y, p0.z);
+    if ((km & 3u) == G::P_MOVING) {
+      float4 p1 = ld4(pp->p1);
+      c = c + ((time - p1.w) / pp->p2[0]) * v3(p1.x, p1.y, p1.z);
+    }
+    rec.mat = km >> 4;
+    Vec3 at = wo + t * wd;
+    Vec3 outward = (at - c) / p0.w;
+    rec.p = at;
+    set_face_normal(rec, wd, outward);
+    return rec;
+  } else {
+    uint32_t parent;
+    if (kind == G::K_MEDIUM) parent = P.media[payload].parent;
+    else parent = P.prims[payload].parent;
+    uint32_t chain[G::MAX_INST_DEPTH];
+    Vec3 dirs[G::MAX_INST_DEPTH];
+    int n = 0;
+    for (uint32_t q = parent; q != G::NONE && n < G::MAX_INST_DEPTH; q = P.insts[q].parent) chain[n++] = q;
+    Vec3 o = wo, d = wd;
+    for (int l = n - 1; l >= 0; l--) {
+      dirs[l] = d;
+      inst_ray(P.insts[chain[l]], o, d);
+    }
+    if (kind == G::K_MEDIUM) {
+      rec.p = o + t * d;
+      rec.n = v3(0.0f, 0.0f, 0.0f);
+      rec.front = false;
+      rec.mat = P.media[payload].mat;
+    } else {
+      const G::Prim* pp = P.prims + payload;
+      const uint32_t km = pp->km;
+      const uint32_t pkind = km & 3u;
+      rec.mat = km >> 4;
+      const bool uv = P.mats[rec.mat].needs_uv != 0;
+      float4 p0 = ld4(pp->p0);
+      if (pkind == G::P_RECT) {
+        int k, a, b;
+        plane_axes((km >> 2) & 3u, k, a, b);
+        float av = o[a] + t * d[a];
+        float bv = o[b] + t * d[b];
+        rec.p = o + t * d;
+        rec.u = (av - p0.x) / pp->p1[1];
+        rec.v = (bv - p0.z) / pp->p1[2];
+        Vec3 outward = v3(0.0f, 0.0f, 0.0f);
+        outward[k] = 1.0f;
+        set_face_normal(rec, d, outward);
+      } else {
+        Vec3 c = v3(p0.x, p0.y, p0.z);
+        if (pkind == G::P_MOVING) {
+          float4 p1 = ld4(pp->p1);
+          c = c + ((time - p1.w) / pp->p2[0]) * v3(p1.x, p1.y, p1.z);
+        }
+        Vec3 at = o + t * d;
+        Vec3 outward = (at - c) / p0.w;
+        if (uv) sphere_uv(outward, rec.u, rec.v);
+        rec.p = at;
+        set_face_normal(rec, d, outward);
+      }
+    }
+    for (int l = 0; l < n; l++) {
+      const G::Inst& in = P.insts[chain[l]];
+      if (in.kind == G::I_TRANSLATE) {
+        rec.p = rec.p + v3(in.d[0], in.d[1], in.d[2]);
+        set_face_normal(rec, dirs[l], rec.n);
+      } else {
+        int a = (int)(in.axis + 1) % 3, b = (int)(in.axis + 2) % 3;
+        float s = in.sin_t, c = in.cos_t;
+        Vec3 p = rec.p, nn = rec.n;
+        p[a] = c * rec.p[a] - s * rec.p[b];
+        p[b] = s * rec.p[a] + c * rec.p[b];
+        nn[a] = c * rec.n[a] - s * rec.n[b];
+        nn[b] = s * rec.n[a] + c * rec.n[b];
+        rec.p = p;
+        rec.n = nn;
+      }
+    }
+    return rec;
+  }
+}
+
+/* perlin_noise.rs:80-123 */
+__device__ float perlin_noise(const G::Perlin* pn, Vec3 point) {
+  int32_t i = sat_f2i32(floorf(point.x));
+  int32_t j = sat_f2i32(floorf(point.y));
+  int32_t k = sat_f2i32(floorf(point.z));
+  float u = point.x - floorf(point.x);
+  float v = point.y - floorf(point.y);
+  float w = point.z - floorf(point.z);
+  u = u * u * (3.0f - 2.0f * u);
+  v = v * v * (3.0f - 2.0f * v);
+  w = w * w * (3.0f - 2.0f * w);
+  float acc = 0.0f;
+#pragma unroll
+  for (int idx = 0; idx < 8; idx++) {
+    const int x = idx / 4, y = (idx / 2) % 2, z = idx % 2;
+    uint32_t px = pn->perm[0][(uint32_t)((i + x) & 255)];
+    uint32_t py = pn->perm[1][(uint32_t)((j + y) & 255)];
+    uint32_t pz = pn->perm[2][(uint32_t)((k + z) & 255)];
+    float4 g = ld4(pn->ranvec[px ^ py ^ pz]);
+    Vec3 weight = v3(u - (float)x, v - (float)y, w - (float)z);
+    acc += ((float)x * u + (float)(1 - x) * (1.0f - u)) * ((float)y * v + (float)(1 - y) * (1.0f - v)) *
+           ((float)z * w + (float)(1 - z) * (1.0f - w)) * dot(v3(g.x, g.y, g.z), weight);
+  }
+  return acc;
+}
+
+/* textures/.rs value() */
+template <bool FULL>
+__device__ Vec3 tex_value(const KParams& P, uint32_t id, float u, float v, Vec3 p) {
+  for (int guard = 0; guard < 64; guard++) {
+    const G::Tex& T = P.texs[id];
+    if (T.kind == G::T_SOLID) return v3(T.a[0], T.a[1], T.a[2]);
+    if (T.kind == G::T_CHECKER) { /* checker_texture.rs:22-29 */
+      float sines = sin_f(10.0f * p.x) * sin_f(10.0f * p.y) * sin_f(10.0f * p.z);
+      id = sines < 0.0f ? T.i0 : T.i1;
+      continue;
+    }
+    if constexpr (FULL) {
+      if (T.kind == G::T_NOISE) { /* noise_texture.rs:24-31 + turbulence perlin_noise.rs:66-78 */
+        const G::Perlin* pn = P.perlin + T.i0;
+        float scale = T.a[0];
+        Vec3 q = scale * p;
+        float accumulator = 0.0f, weight = 1.0f;
+        for (int o = 0; o < 7; o++) {
+          accumulator += weight * perlin_noise(pn, q);
+          weight *= 0.5f;
+          q = q * 2.0f;
+        }
+        float s = 1.0f + sin_f((scale * p.z) + (10.0f * fabsf(accumulator)));
+        return (v3(1.0f, 1.0f, 1.0f) * 0.5f) * s;
+      }
+      if (T.kind == G::T_IMAGE) { /* image_texture.rs:36-62 */
+        if (T.i1 == 0) return v3(1.0f, 0.0f, 1.0f);
+        float uu = u < 0.0f ? 0.0f : (u > 1.0f ? 1.0f : u);
+        float vc = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
+        float vv = 1.0f - vc;
+        uint32_t ii = sat_f2u32(uu * (float)T.i1);
+        uint32_t jj = sat_f2u32(vv * (float)T.i2);
+        if (ii >= T.i1) ii = T.i1 - 1;
+        if (jj >= T.i2) jj = T.i2 - 1;
+        const uint8_t* px = P.images + T.i0 + ((size_t)jj * T.i1 + ii) * T.i3;
+        const float cs = 1.0f / 255.0f;
+        return v3(cs * (float)px[0], cs * (float)px[1], cs * (float)px[2]);
+      }
+    }
+    break;
+  }
+  return v3(0.0f, 0.0f, 0.0f);
+}
+
+/* ------------------------------------------------------------------ the megakernel */
+template <int CULL, bool FULL>
+__global__ __launch_bounds__(256) void render_kernel(KParams P) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const float scale = 1.0f / (float)P.spp; /* application.rs:403 */
+  const float inf = __uint_as_float(0x7f800000u);
+
+  bool has_pixel = false, exhausted = false, in_path = false;
+  uint32_t px = 0, py = 0, out_idx = 0, sample = 0;
+  Vec3 sum = v3(0.0f, 0.0f, 0.0f);
+  Rng rng;
+  rng.s0 = rng.s1 = rng.s2 = rng.s3 = 1u;
+  PathKey pk{0ull, 0u};
+  uint32_t depth_left = 0;
+  Vec3 ro = v3(0.0f, 0.0f, 0.0f), rd = v3(0.0f, 0.0f, 1.0f);
+  float rtime = 0.0f;
+  Vec3 thr = v3(1.0f, 1.0f, 1.0f), rad = v3(0.0f, 0.0f, 0.0f);
+  uint32_t n_seg = 0, n_samples = 0, n_pixels = 0;
+
+  for (;;) {
+    /* ---- claim pixels for idle lanes: one atomic per wave ---- */
+    const bool want = !has_pixel && !exhausted;
+    const unsigned long long want_mask = __ballot(want);
+    if (want_mask) {
+      const uint32_t cnt = (uint32_t)__popcll(want_mask);
+      const int leader = __ffsll((long long)want_mask) - 1;
+      uint32_t base = 0;
+      if ((int)lane == leader) base = atomicAdd(P.counter, cnt);
+      base = __shfl(base, leader);
+      if (want) {
+        const uint32_t rank = (uint32_t)__popcll(want_mask & ((1ull << lane) - 1ull));
+        const uint32_t w = base + rank;
+        if (w >= P.total_work) {
+          exhausted = true;
+        } else {
+          /* tile lookup (binary search on pad_start) then 8x8 block order inside the tile */
+          uint32_t lo = 0, hi = P.n_tiles - 1;
+          while (lo < hi) {
+            uint32_t mid = (lo + hi + 1) >> 1;
+            if (P.tiles[mid].pad_start <= w) lo = mid; else hi = mid - 1;
+          }
+          const G::TileDev T = P.tiles[lo];
+          const uint32_t q = w - T.pad_start, blk = q >> 6, in = q & 63u;
+          const uint32_t lx = (blk % T.bw) * 8u + (in & 7u), ly = (blk / T.bw) * 8u + (in >> 3);
+          if (lx < T.w && ly < T.h) {
+            has_pixel = true;
+            px = T.x + lx;
+            py = T.y + ly;
+            out_idx = T.out_off + ly * T.w + lx;
+            sample = 0;
+            sum = v3(0.0f, 0.0f, 0.0f);
+            in_path = false;
+          }
+        }
+      }
+    }
+    if (!__any(has_pixel || !exhausted)) break;
+    if (!has_pixel) continue;
+
+    /* ---- start the next sample (application.rs:444-447, camera.rs:85-95) ---- */
+    if (!in_path) {
+      pk.pkey = path_key(P.seed, py * P.W + px, P.sample_offset + sample);
+      pk.segment = 0;
+      rng = rng_from_key(pk.pkey);
+      float u = ((float)px + rng.gen_f32()) / ((float)P.W - 1.0f);
+      float v = ((float)py + rng.gen_f32()) / ((float)P.H - 1.0f);
+      Vec3 disk = random_in_unit_disk(rng);
+      rtime = rng.gen_range_f32(P.time0, P.time1);
+      Vec3 rdk = P.lens_radius * disk;
+      Vec3 offset = P.cam_u * rdk.x + P.cam_vv * rdk.y;
+      ro = P.cam_origin + offset;
+      rd = (((P.cam_llc + u * P.cam_h) + v * P.cam_v) - P.cam_origin) - offset;
+      thr = v3(1.0f, 1.0f, 1.0f);
+      rad = v3(0.0f, 0.0f, 0.0f);
+      depth_left = P.max_depth;
+      in_path = true;
+    }
+
+    /* ---- one segment of ray_color (application.rs:477-495) ---- */
+    bool done = false;
+    if (depth_left == 0) {
+      done = true; /* depth cap: black (:478-480) */
+    } else {
+      float closest = inf;
+      uint32_t winner = G::NONE;
+      trace<CULL, FULL, FULL>(P, 0u, P.main_end, ro, rd, rtime, P.t_min, closest, winner, pk);
+      n_seg++;
+      pk.segment++;
+      if (winner == G::NONE) {
+        rad = rad + mul_elem(thr, P.background);
+        done = true;
+      } else {
+        Rec rec = make_record<FULL>(P, winner, closest, ro, rd, rtime);
+        const G::Mat M = P.mats[rec.mat];
+        Vec3 emitted = v3(0.0f, 0.0f, 0.0f);
+        Vec3 att = v3(0.0f, 0.0f, 0.0f), ndir = v3(0.0f, 0.0f, 0.0f);
+        bool scattered = false;
+        if (M.kind == G::M_LAMBERTIAN) { /* lambertian.rs:27-38 */
+          ndir = rec.n + random_unit_vector(rng);
+          if (near_zero(ndir)) ndir = rec.n;
+          att = tex_value<FULL>(P, M.tex, rec.u, rec.v, rec.p);
+          scattered = true;
+        } else if (M.kind == G::M_METAL) { /* metal.rs:29-42 */
+          Vec3 reflected = reflect(normalize(rd), rec.n);
+          ndir = reflected + M.a[3] * random_in_unit_sphere(rng);
+          scattered = dot(ndir, rec.n) > 0.0f;
+          att = v3(M.a[0], M.a[1], M.a[2]);
+        } else if (M.kind == G::M_DIELECTRIC) { /* dielectric.rs:31-55 */
+          float ratio = rec.front ? (1.0f / M.a[0]) : M.a[0];
+          Vec3 ud = normalize(rd);
+          float cos_theta = min_rs(dot(-ud, rec.n), 1.0f);
+          float sin_theta = sqrtf(1.0f - cos_theta * cos_theta);
+          bool cannot_refract = (ratio * sin_theta) > 1.0f;
+          if (cannot_refract || reflectance(cos_theta, ratio) > rng.gen_f32()) ndir = reflect(ud, rec.n);
+          else ndir = refract(ud, rec.n, ratio);
+          att = v3(1.0f, 1.0f, 1.0f);
+          scattered = true;
+        } else if (FULL && M.kind == G::M_DIFFUSE_LIGHT) { /* diffuse_light.rs:20-28 */
+          emitted = tex_value<FULL>(P, M.tex, rec.u, rec.v, rec.p);
+        } else if (FULL && M.kind == G::M_ISOTROPIC) { /* isotropic.rs:26-33 */
+          att = tex_value<FULL>(P, M.tex, rec.u, rec.v, rec.p);
+          ndir = random_in_unit_sphere(rng);
+          scattered = true;
+        }
+        /* L = emitted + att * L_next, accumulated front to back */
+        rad = rad + mul_elem(thr, emitted);
+        if (scattered) {
+          thr = mul_elem(thr, att);
+          ro = rec.p;
+          rd = ndir;
+          depth_left--;
+        } else {
+          done = true;
+        }
+      }
+    }
+    if (done) {
+      sum = sum + rad;
+      in_path = false;
+      n_samples++;
+      if (++sample == P.spp) {
+        P.out[out_idx] = make_float4(sqrtf(sum.x * scale), sqrtf(sum.y * scale), sqrtf(sum.z * scale), 1.0f);
+        has_pixel = false;
+        n_pixels++;
+      }
+    }
+  }
+  atomicAdd(&P.stats[0], (unsigned long long)n_seg);
+  atomicAdd(&P.stats[1], (unsigned long long)n_samples);
+  atomicAdd(&P.stats[2], (unsigned long long)n_pixels);
+}
+
+__global__ void math_kernel(int op, const float* x, const float* y, float* out, uint32_t n) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float a = x[i], b = y ? y[i] : 0.0f, r = 0.0f;
+  switch (op) {
+    case 0: r = sin_f(a); break;
+    case 1: r = cos_f(a); break;
+    case 2: r = acos_f(a); break;
+    case 3: r = atan2_f(a, b); break;
+    case 4: r = ln_f(a); break;
+    case 5: r = pow5_f(a); break;
+    case 6: r = tan_f(a); break;
+  }
+  out[i] = r;
+}
+
+/* ------------------------------------------------------------------ host helpers */
+struct HipError {
+  hrt_status code;
+  std::string msg;
+};
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw HipError{HRT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e)};
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    hip_check(hipGetDevice(&prev), "hipGetDevice");
+    if (dev >= 0 && dev != prev) hip_check(hipSetDevice(dev), "hipSetDevice");
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+template <class F>
+hrt_status hguard(F&& f) {
+  try {
+    f();
+    return HRT_OK;
+  } catch (const HipError& e) {
+    set_error(e.msg);
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    set_error("out of host memory");
+    return HRT_ERR_OOM;
+  } catch (const std::exception& e) {
+    set_error(e.what());
+    return HRT_ERR_INVALID_ARG;
+  }
+}
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+template <int CULL, bool FULL>
+int resident_grid(int device) {
+  static int cached[64] = {0};
+  if (device >= 0 && device < 64 && cached[device]) return cached[device];
+  int per_cu = 0;
+  hip_check(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_kernel<CULL, FULL>, 256, 0),
+            "hipOccupancyMaxActiveBlocksPerMultiprocessor");
+  hipDeviceProp_t prop;
+  hip_check(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
+  int g = std::max(1, per_cu) * prop.multiProcessorCount;
+  if (device >= 0 && device < 64) cached[device] = g;
+  return g;
+}
+
+template <int CULL, bool FULL>
+void launch(const KParams& kp, int device, hipStream_t stream) {
+  int grid = resident_grid<CULL, FULL>(device);
+  hipLaunchKernelGGL((render_kernel<CULL, FULL>), dim3(grid), dim3(256), 0, stream, kp);
+  hip_check(hipGetLastError(), "render_kernel launch");
+}
+
+}  // namespace
+
+/* ============================================================================ device runtime */
+namespace hrt {
+
+hrt_status device_upload(hrt_scene* s, int device) {
+  return hguard([&] {
+    if (device < 0) hip_check(hipGetDevice(&device), "hipGetDevice");
+    DeviceGuard dg(device);
+    device_release(s);
+    size_t off = 0;
+    auto section = [&](size_t bytes) {
+      size_t o = off;
+      off = align256(off + std::max<size_t>(bytes, 16));
+      return o;
+    };
+    s->off_nodes = section(s->g_nodes.size() * sizeof(G::Node));
+    s->off_prims = section(s->g_prims.size() * sizeof(G::Prim));
+    s->off_insts = section(s->g_insts.size() * sizeof(G::Inst));
+    s->off_media = section(s->g_media.size() * sizeof(G::Medium));
+    s->off_mats = section(s->g_mats.size() * sizeof(G::Mat));
+    s->off_texs = section(s->g_texs.size() * sizeof(G::Tex));
+    s->off_perlin = section(s->perlin.size() * sizeof(G::Perlin));
+    s->off_images = section(s->images.size());
+    s->blob_bytes = off;
+    std::vector<uint8_t> blob(off, 0);
+    auto put = [&](size_t o, const void* src, size_t bytes) {
+      if (bytes) memcpy(blob.data() + o, src, bytes);
+    };
+    put(s->off_nodes, s->g_nodes.data(), s->g_nodes.size() * sizeof(G::Node));
+    put(s->off_prims, s->g_prims.data(), s->g_prims.size() * sizeof(G::Prim));
+    put(s->off_insts, s->g_insts.data(), s->g_insts.size() * sizeof(G::Inst));
+    put(s->off_media, s->g_media.data(), s->g_media.size() * sizeof(G::Medium));
+    put(s->off_mats, s->g_mats.data(), s->g_mats.size() * sizeof(G::Mat));
+    put(s->off_texs, s->g_texs.data(), s->g_texs.size() * sizeof(G::Tex));
+    put(s->off_perlin, s->perlin.data(), s->perlin.size() * sizeof(G::Perlin));
+    put(s->off_images, s->images.data(), s->images.size());
+    hip_check(hipMalloc(&s->d_blob, off), "hipMalloc(scene)");
+    hip_check(hipMemcpy(s->d_blob, blob.data(), off, hipMemcpyHostToDevice), "hipMemcpy(scene)");
+    s->device = device;
+  });
+}
+
+void device_release(hrt_scene* s) {
+  if (!s || s->device < 0) return;
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  (void)hipSetDevice(s->device);
+  if (s->d_blob) (void)hipFree(s->d_blob);
+  s->d_blob = nullptr;
+  if (prev >= 0) (void)hipSetDevice(prev);
+  s->device = -1;
+}
+
+}  // namespace hrt
+
+extern "C" {
+
+hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hrt_render_params* p,
+                                   const hrt_tile* tiles, uint32_t n_tiles, float* d_rgba, void* stream_,
+                                   hrt_render_stats* stats) {
+  return hguard([&] {
+    if (!s || !cam || !p || !tiles || !d_rgba || n_tiles == 0)
+      throw HipError{HRT_ERR_INVALID_ARG, "hrt_render_tiles_device: null argument"};
+    if (!s->committed || !s->d_blob) throw HipError{HRT_ERR_STATE, "scene not committed"};
+    if (p->width < 2 || p->height < 2 || p->samples == 0 || p->flags != 0)
+      throw HipError{HRT_ERR_INVALID_ARG, "bad render params (width/height >= 2, samples > 0, flags == 0)"};
+    if (!(cam->time0 < cam->time1)) throw HipError{HRT_ERR_INVALID_ARG, "camera time0 must be < time1"};
+    std::vector<G::TileDev> td(n_tiles);
+    uint64_t pad = 0, outp = 0;
+    for (uint32_t i = 0; i < n_tiles; i++) {
+      const hrt_tile& t = tiles[i];
+      if (t.w == 0 || t.h == 0 || (uint64_t)t.x + t.w > p->width || (uint64_t)t.y + t.h > p->height)
+        throw HipError{HRT_ERR_INVALID_ARG, "tile outside the image"};
+      uint32_t bw = (t.w + 7) / 8, bh = (t.h + 7) / 8;
+      td[i] = G::TileDev{t.x, t.y, t.w, t.h, bw, (uint32_t)pad, (uint32_t)outp, 0};
+      pad += (uint64_t)bw * bh * 64;
+      outp += (uint64_t)t.w * t.h;
+    }
+    if (pad >= 0xFFFF0000ull) throw HipError{HRT_ERR_UNSUPPORTED, "more than 4G pixels in one call"};
+    hipStream_t stream = (hipStream_t)stream_;
+    DeviceGuard dg(s->device);
+    /* per-call scratch: [counter u32 | pad | stats 3 x u64] + tiles, stream-ordered */
+    size_t tiles_bytes = n_tiles * sizeof(G::TileDev);
+    void* scratch = nullptr;
+    hip_check(hipMallocAsync(&scratch, 64 + tiles_bytes, stream), "hipMallocAsync");
+    hip_check(hipMemsetAsync(scratch, 0, 64, stream), "hipMemsetAsync");
+    hip_check(hipMemcpyAsync((uint8_t*)scratch + 64, td.data(), tiles_bytes, hipMemcpyHostToDevice, stream),
+              "hipMemcpyAsync(tiles)");
+    KParams kp;
+    uint8_t* base = (uint8_t*)s->d_blob;
+    kp.nodes = (const G::Node*)(base + s->off_nodes);
+    kp.prims = (const G::Prim*)(base + s->off_prims);
+    kp.insts = (const G::Inst*)(base + s->off_insts);
+    kp.media = (const G::Medium*)(base + s->off_media);
+    kp.mats = (const G::Mat*)(base + s->off_mats);
+    kp.texs = (const G::Tex*)(base + s->off_texs);
+    kp.perlin = (const G::Perlin*)(base + s->off_perlin);
+    kp.images = (const uint8_t*)(base + s->off_images);
+    kp.main_end = s->main_end;
+    kp.ln_e = s->ln_e;
+    kp.cam_origin = v3(cam->origin[0], cam->origin[1], cam->origin[2]);
+    kp.cam_llc = v3(cam->lower_left_corner[0], cam->lower_left_corner[1], cam->lower_left_corner[2]);
+    kp.cam_h = v3(cam->horizontal[0], cam->horizontal[1], cam->horizontal[2]);
+    kp.cam_v = v3(cam->vertical[0], cam->vertical[1], cam->vertical[2]);
+    kp.cam_u = v3(cam->u[0], cam->u[1], cam->u[2]);
+    kp.cam_vv = v3(cam->v[0], cam->v[1], cam->v[2]);
+    kp.lens_radius = cam->lens_radius;
+    kp.time0 = cam->time0;
+    kp.time1 = cam->time1;
+    kp.W = p->width;
+    kp.H = p->height;
+    kp.spp = p->samples;
+    kp.max_depth = p->max_depth;
+    kp.sample_offset = p->sample_offset;
+    kp.t_min = p->t_min;
+    kp.background = v3(p->background[0], p->background[1], p->background[2]);
+    kp.seed = p->seed;
+    kp.tiles = (const G::TileDev*)((uint8_t*)scratch + 64);
+    kp.n_tiles = n_tiles;
+    kp.total_work = (uint32_t)pad;
+    kp.out = (float4*)d_rgba;
+    kp.counter = (uint32_t*)scratch;
+    kp.stats = (unsigned long long*)((uint8_t*)scratch + 8);
+    const bool full = (s->feature_mask & ~G::F_BASIC) != 0;
+    if (s->cull_mode == G::CULL_SLAB) {
+      if (full) launch<G::CULL_SLAB, true>(kp, s->device, stream);
+      else launch<G::CULL_SLAB, false>(kp, s->device, stream);
+    } else {
+      if (full) launch<G::CULL_REFERENCE, true>(kp, s->device, stream);
+      else launch<G::CULL_REFERENCE, false>(kp, s->device, stream);
+    }
+    if (stats) {
+      unsigned long long h[3];
+      hip_check(hipMemcpyAsync(h, (uint8_t*)scratch + 8, sizeof(h), hipMemcpyDeviceToHost, stream),
+                "hipMemcpyAsync(stats)");
+      hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+      stats->segments = h[0];
+      stats->samples = h[1];
+      stats->pixels = h[2];
+    }
+    hip_check(hipFreeAsync(scratch, stream), "hipFreeAsync");
+  });
+}
+
+hrt_status hrt_render_device(hrt_scene* s, const hrt_camera* cam, const hrt_render_params* p, uint32_t x0,
+                             uint32_t y0, uint32_t w, uint32_t h, float* d_rgba, void* stream,
+                             hrt_render_stats* stats) {
+  hrt_tile t{x0, y0, w, h};
+  return hrt_render_tiles_device(s, cam, p, &t, 1, d_rgba, stream, stats);
+}
+
+hrt_status hrt_render(hrt_scene* s, const hrt_camera* cam, const hrt_render_params* p, uint32_t x0,
+                      uint32_t y0, uint32_t w, uint32_t h, float* rgba_out, hrt_render_stats* stats) {
+  if (!s || !rgba_out || !s->committed) {
+    set_error("hrt_render: null argument or scene not committed");
+    return (s && !s->committed) ? HRT_ERR_STATE : HRT_ERR_INVALID_ARG;
+  }
+  float* d_out = nullptr;
+  hrt_status st = hguard([&] {
+    DeviceGuard dg(s->device);
+    hip_check(hipMalloc((void**)&d_out, (size_t)w * h * 16 + 16), "hipMalloc(out)");
+  });
+  if (st != HRT_OK) return st;
+  hrt_render_stats local;
+  st = hrt_render_device(s, cam, p, x0, y0, w, h, d_out, nullptr, stats ? stats : &local);
+  if (st == HRT_OK) {
+    st = hguard([&] {
+      DeviceGuard dg(s->device);
+      hip_check(hipMemcpy(rgba_out, d_out, (size_t)w * h * 16, hipMemcpyDeviceToHost), "hipMemcpy(out)");
+    });
+  }
+  {
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(s->device);
+    (void)hipFree(d_out);
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  return st;
+}
+
+hrt_status hrt_debug_device_math(int32_t op, const float* x, const float* y, float* out, uint32_t n) {
+  return hguard([&] {
+    if (!x || !out || op < 0 || op > 6) throw HipError{HRT_ERR_INVALID_ARG, "bad argument"};
+    if (n == 0) return;
+    float *dx = nullptr, *dy = nullptr, *dout = nullptr;
+    hip_check(hipMalloc((void**)&dx, n * 4), "hipMalloc");
+    hip_check(hipMalloc((void**)&dout, n * 4), "hipMalloc");
+    if (y) hip_check(hipMalloc((void**)&dy, n * 4), "hipMalloc");
+    hip_check(hipMemcpy(dx, x, n * 4, hipMemcpyHostToDevice), "hipMemcpy");
+    if (y) hip_check(hipMemcpy(dy, y, n * 4, hipMemcpyHostToDevice), "hipMemcpy");
+    hipLaunchKernelGGL(math_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, op, dx, dy, dout, n);
+    hip_check(hipGetLastError(), "math_kernel launch");
+    hip_check(hipMemcpy(out, dout, n * 4, hipMemcpyDeviceToHost), "hipMemcpy");
+    (void)hipFree(dx);
+    (void)hipFree(dout);
+    if (dy) (void)hipFree(dy);
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,830 @@
+/*
+ * scene.cpp — the host half of libhrt: scene-graph constructors of the C ABI, BvhNode::new,
+ * bounding boxes / counts with the reference's semantics, Camera::new/resize, the tile grid and the
+ * lowering of the graph into the pre-order device layout (layout.h).
+ *
+ * Reference semantics kept here (paths in SkillerRaptor/hyper-ray-tracer):
+ *   bounding boxes   sphere.rs:78-83, moving_sphere.rs:98-110, rect.rs:88-103 (incl. the ZX box whose
+ *                    x/z ranges are swapped relative to the hit test at rect.rs:57), cuboid.rs:104-106,
+ *                    translation.rs:40-48, rotation.rs:41-99 (computed once over t in [0, 1]),
+ *                    constant_medium.rs:78-80, list.rs:33-44, bvh_node.rs:129-131
+ *   BVH build        bvh_node.rs:27-101 (longest axis, min+max key, upper half right, 1 prim/leaf)
+ *   counts           hittable/.rs count() (Rotation::count == 1, rotation.rs:140-142)
+ */
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "scene_internal.h"
+
+using namespace hrt;
+using namespace hrt::host;
+namespace G = hrt::gpu;
+
+namespace hrt {
+static thread_local std::string g_error;
+void set_error(const std::string& msg) { g_error = msg; }
+}  // namespace hrt
+
+namespace {
+
+struct Error : std::runtime_error {
+  hrt_status code;
+  Error(hrt_status c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+template <class F>
+hrt_status guard(F&& f) {
+  try {
+    f();
+    return HRT_OK;
+  } catch (const Error& e) {
+    set_error(e.what());
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    set_error("out of host memory");
+    return HRT_ERR_OOM;
+  } catch (const std::exception& e) {
+    set_error(e.what());
+    return HRT_ERR_INVALID_ARG;
+  }
+}
+
+void need(bool c, hrt_status code, const char* msg) {
+  if (!c) throw Error(code, msg);
+}
+void mutable_scene(hrt_scene* s) {
+  need(s != nullptr, HRT_ERR_INVALID_ARG, "null scene");
+  need(!s->committed, HRT_ERR_STATE, "scene is immutable after hrt_scene_commit");
+}
+void check_tex(const hrt_scene* s, uint32_t t) {
+  need(t < s->texs.size(), HRT_ERR_INVALID_ARG, "bad texture id");
+}
+void check_mat(const hrt_scene* s, uint32_t m) {
+  need(m < s->mats.size(), HRT_ERR_INVALID_ARG, "bad material id");
+}
+uint32_t take_child(hrt_scene* s, uint32_t c) {
+  need(c < s->nodes.size(), HRT_ERR_INVALID_ARG, "bad node id");
+  need(!s->nodes[c].owned, HRT_ERR_INVALID_ARG, "node already owned by another node");
+  s->nodes[c].owned = true;
+  return c;
+}
+uint32_t push_node(hrt_scene* s, HNode&& n) {
+  s->nodes.push_back(std::move(n));
+  return (uint32_t)(s->nodes.size() - 1);
+}
+Vec3 vin(const float* p) {
+  need(p != nullptr, HRT_ERR_INVALID_ARG, "null vector");
+  return v3(p[0], p[1], p[2]);
+}
+
+/* aabb.rs:49-63 */
+Aabb surrounding(const Aabb& a, const Aabb& b) {
+  return Aabb{v3(fminf(a.mn.x, b.mn.x), fminf(a.mn.y, b.mn.y), fminf(a.mn.z, b.mn.z)),
+              v3(fmaxf(a.mx.x, b.mx.x), fmaxf(a.mx.y, b.mx.y), fmaxf(a.mx.z, b.mx.z))};
+}
+
+/* moving_sphere.rs:53-59 */
+Vec3 moving_center(const HNode& n, float time) {
+  return n.c0 + ((time - n.t0) / (n.t1 - n.t0)) * (n.c1 - n.c0);
+}
+
+bool bbox(const hrt_scene* s, uint32_t id, float t0, float t1, Aabb& out) {
+  const HNode& n = s->nodes[id];
+  switch (n.kind) {
+    case N_SPHERE: {
+      Vec3 rv = v3(n.r, n.r, n.r);
+      out = Aabb{n.c0 - rv, n.c0 + rv};
+      return true;
+    }
+    case N_MOVING: {
+      Vec3 rv = v3(n.r, n.r, n.r);
+      Aabb b0{moving_center(n, t0) - rv, moving_center(n, t0) + rv};
+      Aabb b1{moving_center(n, t1) - rv, moving_center(n, t1) + rv};
+      out = surrounding(b0, b1);
+      return true;
+    }
+    case N_RECT:
+      if (n.plane == HRT_PLANE_XY) out = Aabb{v3(n.a0, n.b0, n.k - 0.0001f), v3(n.a1, n.b1, n.k + 0.0001f)};
+      else if (n.plane == HRT_PLANE_YZ) out = Aabb{v3(n.k - 0.0001f, n.a0, n.b0), v3(n.k + 0.0001f, n.a1, n.b1)};
+      else out = Aabb{v3(n.a0, n.k - 0.0001f, n.b0), v3(n.a1, n.k + 0.0001f, n.b1)};
+      return true;
+    case N_CUBOID:
+      out = n.box;
+      return true;
+    case N_TRANSLATE: {
+      Aabb b;
+      if (!bbox(s, n.children[0], t0, t1, b)) return false;
+      out = Aabb{b.mn + n.disp, b.mx + n.disp};
+      return true;
+    }
+    case N_ROTATE:
+      if (!n.has_box) return false;
+      out = n.box;
+      return true;
+    case N_MEDIUM:
+      return bbox(s, n.children[0], t0, t1, out);
+    case N_LIST: {
+      if (n.children.empty()) return false;
+      Aabb acc;
+      if (!bbox(s, n.children[0], t0, t1, acc)) return false;
+      for (size_t i = 1; i < n.children.size(); i++) {
+        Aabb b;
+        if (!bbox(s, n.children[i], t0, t1, b)) return false;
+        acc = surrounding(acc, b);
+      }
+      out = acc;
+      return true;
+    }
+    case N_BVH:
+      out = n.box;
+      return true;
+  }
+  return false;
+}
+
+uint32_t count(const hrt_scene* s, uint32_t id) {
+  const HNode& n = s->nodes[id];
+  switch (n.kind) {
+    case N_SPHERE: case N_MOVING: case N_RECT: case N_ROTATE:
+      return 1;
+    case N_TRANSLATE: case N_MEDIUM:
+      return count(s, n.children[0]);
+    case N_CUBOID: case N_LIST: case N_BVH: {
+      uint32_t c = 0;
+      for (uint32_t ch : n.children) c += count(s, ch);
+      return c;
+    }
+  }
+  return 0;
+}
+
+/* bvh_node.rs:27-63.  Rust's sort_unstable_by is an insertion sort (stable) below 21 elements and
+ * pdqsort above; a stable sort reproduces the former exactly and fixes an order for key ties in the
+ * latter (closest hits do not depend on it). */
+uint32_t build_bvh(hrt_scene* s, std::vector<uint32_t> objects, float t0, float t1) {
+  need(!objects.empty(), HRT_ERR_EMPTY, "no elements in scene (BvhNode::new with no objects)");
+  float ranges[3];
+  for (int a = 0; a < 3; a++) {
+    float mn = 3.40282347e+38f, mx = -3.40282347e+38f;
+    for (uint32_t o : objects) {
+      Aabb b;
+      if (!bbox(s, o, t0, t1, b)) continue;
+      mn = fminf(mn, b.mn[a]);
+      mx = fmaxf(mx, b.mx[a]);
+    }
+    ranges[a] = mx - mn;
+    need(ranges[a] == ranges[a], HRT_ERR_NAN, "NaN axis range in BVH build");
+  }
+  int order[3] = {0, 1, 2};
+  std::stable_sort(order, order + 3, [&](int a, int b) { return ranges[a] > ranges[b]; });
+  int axis = order[0];
+  std::vector<std::pair<float, uint32_t>> keys;
+  keys.reserve(objects.size());
+  for (uint32_t o : objects) {
+    Aabb b;
+    need(bbox(s, o, t0, t1, b), HRT_ERR_NO_BBOX, "object without bounding box inside a BVH");
+    float key = b.mn[axis] + b.mx[axis];
+    need(key == key, HRT_ERR_NAN, "NaN bounding box inside a BVH");
+    keys.emplace_back(key, o);
+  }
+  std::stable_sort(keys.begin(), keys.end(),
+                   [](const std::pair<float, uint32_t>& a, const std::pair<float, uint32_t>& b) {
+                     return a.first < b.first;
+                   });
+  HNode n;
+  n.kind = N_BVH;
+  n.has_box = true;
+  size_t len = keys.size();
+  if (len == 1) {
+    n.children.push_back(keys[0].second);
+    need(bbox(s, keys[0].second, t0, t1, n.box), HRT_ERR_NO_BBOX, "object without bounding box");
+    return push_node(s, std::move(n));
+  }
+  std::vector<uint32_t> lower, upper;
+  for (size_t i = 0; i < len; i++) (i < len / 2 ? lower : upper).push_back(keys[i].second);
+  uint32_t right = build_bvh(s, std::move(upper), t0, t1);
+  uint32_t left = build_bvh(s, std::move(lower), t0, t1);
+  n.box = surrounding(s->nodes[left].box, s->nodes[right].box);
+  n.children = {left, right};
+  for (uint32_t c : n.children) s->nodes[c].owned = true;
+  return push_node(s, std::move(n));
+}
+
+/* ------------------------------------------------------------------ lowering (commit) */
+struct Flattener {
+  hrt_scene* s;
+  struct PendingMedium {
+    uint32_t medium;
+    uint32_t boundary;
+  };
+  std::vector<PendingMedium> pending;
+  bool in_boundary = false;
+  int inst_depth = 0, max_inst_depth = 0;
+
+  uint32_t emit_node(uint32_t kind, uint32_t payload, const Aabb* box) {
+    G::Node g;
+    memset(&g, 0, sizeof(g));
+    if (box) {
+      for (int a = 0; a < 3; a++) {
+        g.mn[a] = box->mn[a];
+        g.mx[a] = box->mx[a];
+      }
+    }
+    g.kp = (kind << 24) | payload;
+    g.skip = (uint32_t)s->g_nodes.size() + 1;
+    need(payload < (1u << 24), HRT_ERR_UNSUPPORTED, "scene too large (payload > 2^24)");
+    s->g_nodes.push_back(g);
+    return (uint32_t)(s->g_nodes.size() - 1);
+  }
+
+  uint32_t emit_prim(uint32_t id, uint32_t parent) {
+    const HNode& n = s->nodes[id];
+    G::Prim p;
+    memset(&p, 0, sizeof(p));
+    p.parent = parent;
+    uint32_t kind = 0;
+    if (n.kind == N_SPHERE) {
+      kind = G::P_SPHERE;
+      p.p0[0] = n.c0.x; p.p0[1] = n.c0.y; p.p0[2] = n.c0.z; p.p0[3] = n.r;
+    } else if (n.kind == N_MOVING) {
+      kind = G::P_MOVING;
+      s->feature_mask |= G::F_MOVING;
+      Vec3 dc = n.c1 - n.c0;
+      p.p0[0] = n.c0.x; p.p0[1] = n.c0.y; p.p0[2] = n.c0.z; p.p0[3] = n.r;
+      p.p1[0] = dc.x; p.p1[1] = dc.y; p.p1[2] = dc.z; p.p1[3] = n.t0;
+      p.p2[0] = n.t1 - n.t0;
+    } else {
+      kind = G::P_RECT;
+      s->feature_mask |= G::F_RECT;
+      p.p0[0] = n.a0; p.p0[1] = n.a1; p.p0[2] = n.b0; p.p0[3] = n.b1;
+      p.p1[0] = n.k; p.p1[1] = n.a1 - n.a0; p.p1[2] = n.b1 - n.b0;
+    }
+    need(n.mat < (1u << 27), HRT_ERR_UNSUPPORTED, "too many materials");
+    p.km = kind | ((uint32_t)n.plane << 2) | (n.mat << 4);
+    s->g_prims.push_back(p);
+    return (uint32_t)(s->g_prims.size() - 1);
+  }
+
+  static bool is_prim(NodeKind k) { return k == N_SPHERE || k == N_MOVING || k == N_RECT; }
+
+  void emit(uint32_t id, uint32_t parent) {
+    const HNode& n = s->nodes[id];
+    switch (n.kind) {
+      case N_BVH: {
+        if (n.children.size() == 1 && is_prim(s->nodes[n.children[0]].kind)) {
+          emit_node(G::K_BOX_PRIM, emit_prim(n.children[0], parent), &n.box);
+          return;
+        }
+        uint32_t me = emit_node(G::K_BOX, 0, &n.box);
+        for (uint32_t c : n.children) emit(c, parent);
+        s->g_nodes[me].skip = (uint32_t)s->g_nodes.size();
+        return;
+      }
+      case N_SPHERE: case N_MOVING: case N_RECT:
+        emit_node(G::K_PRIM, emit_prim(id, parent), nullptr);
+        return;
+      case N_CUBOID: case N_LIST:
+        for (uint32_t c : n.children) emit(c, parent);
+        return;
+      case N_TRANSLATE: case N_ROTATE: {
+        G::Inst in;
+        memset(&in, 0, sizeof(in));
+        in.kind = n.kind == N_TRANSLATE ? G::I_TRANSLATE : G::I_ROTATE;
+        in.d[0] = n.disp.x; in.d[1] = n.disp.y; in.d[2] = n.disp.z;
+        in.sin_t = n.sin_t; in.cos_t = n.cos_t;
+        in.axis = (uint32_t)n.axis;
+        in.parent = parent;
+        s->g_insts.push_back(in);
+        uint32_t iid = (uint32_t)(s->g_insts.size() - 1);
+        s->feature_mask |= G::F_INSTANCE;
+        inst_depth++;
+        max_inst_depth = std::max(max_inst_depth, inst_depth);
+        need(inst_depth <= G::MAX_INST_DEPTH, HRT_ERR_UNSUPPORTED, "instances nested deeper than 8");
+        emit_node(G::K_INST_BEGIN, iid, nullptr);
+        emit(n.children[0], iid);
+        emit_node(G::K_INST_END, iid, nullptr);
+        inst_depth--;
+        return;
+      }
+      case N_MEDIUM: {
+        need(!in_boundary, HRT_ERR_UNSUPPORTED, "ConstantMedium inside a medium boundary");
+        G::Medium m;
+        memset(&m, 0, sizeof(m));
+        m.neg_inv_density = n.neg_inv_density;
+        m.medium_id = n.medium_id;
+        m.parent = parent;
+        /* the Isotropic phase function is a material of its own (constant_medium.rs:28) */
+        G::Mat gm;
+        memset(&gm, 0, sizeof(gm));
+        gm.kind = G::M_ISOTROPIC;
+        gm.tex = n.tex;
+        gm.needs_uv = 0;
+        m.mat = (uint32_t)s->g_mats.size();
+        s->g_mats.push_back(gm);
+        s->g_media.push_back(m);
+        uint32_t mid = (uint32_t)(s->g_media.size() - 1);
+        s->feature_mask |= G::F_MEDIUM | G::F_ISOTROPIC;
+        emit_node(G::K_MEDIUM, mid, nullptr);
+        pending.push_back({mid, n.children[0]});
+        return;
+      }
+    }
+  }
+};
+
+bool tex_needs_uv(const hrt_scene* s, uint32_t t, int depth = 0) {
+  if (depth > 64) return true;
+  const HTex& x = s->texs[t];
+  if (x.kind == G::T_IMAGE) return true;
+  if (x.kind == G::T_CHECKER) return tex_needs_uv(s, x.odd, depth + 1) || tex_needs_uv(s, x.even, depth + 1);
+  return false;
+}
+
+uint32_t tex_features(const hrt_scene* s, uint32_t t, int depth = 0) {
+  if (depth > 64) throw Error(HRT_ERR_INVALID_ARG, "texture cycle");
+  const HTex& x = s->texs[t];
+  if (x.kind == G::T_NOISE) return G::F_NOISE;
+  if (x.kind == G::T_IMAGE) return G::F_IMAGE;
+  if (x.kind == G::T_CHECKER)
+    return G::F_CHECKER | tex_features(s, x.odd, depth + 1) | tex_features(s, x.even, depth + 1);
+  return 0;
+}
+
+void flatten(hrt_scene* s) {
+  s->g_nodes.clear(); s->g_prims.clear(); s->g_insts.clear(); s->g_media.clear();
+  s->g_mats.clear(); s->g_texs.clear();
+  s->feature_mask = 0;
+  /* materials and textures first (media append their isotropic materials after these) */
+  for (const HMat& m : s->mats) {
+    G::Mat g;
+    memset(&g, 0, sizeof(g));
+    g.kind = m.kind;
+    g.tex = m.tex == G::NONE ? 0 : m.tex;
+    if (m.kind == G::M_METAL) {
+      g.a[0] = m.albedo.x; g.a[1] = m.albedo.y; g.a[2] = m.albedo.z; g.a[3] = m.fuzz;
+      s->feature_mask |= G::F_METAL;
+    } else if (m.kind == G::M_DIELECTRIC) {
+      g.a[0] = m.ior;
+      s->feature_mask |= G::F_DIELECTRIC;
+    } else {
+      g.needs_uv = tex_needs_uv(s, m.tex) ? 1u : 0u;
+      s->feature_mask |= tex_features(s, m.tex);
+      if (m.kind == G::M_DIFFUSE_LIGHT) s->feature_mask |= G::F_LIGHT;
+      if (m.kind == G::M_ISOTROPIC) s->feature_mask |= G::F_ISOTROPIC;
+    }
+    s->g_mats.push_back(g);
+  }
+  for (const HTex& t : s->texs) {
+    G::Tex g;
+    memset(&g, 0, sizeof(g));
+    g.kind = t.kind;
+    if (t.kind == G::T_SOLID) { g.a[0] = t.color.x; g.a[1] = t.color.y; g.a[2] = t.color.z; }
+    else if (t.kind == G::T_CHECKER) { g.i0 = t.odd; g.i1 = t.even; }
+    else if (t.kind == G::T_NOISE) { g.a[0] = t.scale; g.i0 = t.perlin; }
+    else { g.i0 = (uint32_t)t.img_off; g.i1 = t.w; g.i2 = t.h; g.i3 = t.c; }
+    s->g_texs.push_back(g);
+  }
+  Flattener f{s, {}, false, 0, 0};
+  f.emit(s->root, G::NONE);
+  s->main_end = (uint32_t)s->g_nodes.size();
+  f.in_boundary = true;
+  for (size_t i = 0; i < f.pending.size(); i++) {
+    uint32_t bstart = (uint32_t)s->g_nodes.size();
+    f.emit(f.pending[i].boundary, G::NONE);
+    s->g_media[f.pending[i].medium].bstart = bstart;
+    s->g_media[f.pending[i].medium].bend = (uint32_t)s->g_nodes.size();
+  }
+  for (const G::Medium& m : s->g_media) s->feature_mask |= tex_features(s, s->g_mats[m.mat].tex);
+  /* A slab test only culls subtrees no accepted hit can come from when every box contains its
+   * geometry; rect boxes do not (ZX swap, edge-on faces) and instances/media change the ray, so
+   * those scenes keep the reference's per-axis test ("culling"). */
+  bool sphere_only = (s->feature_mask & (G::F_RECT | G::F_INSTANCE | G::F_MEDIUM)) == 0;
+  s->cull_mode = sphere_only ? G::CULL_SLAB : G::CULL_REFERENCE;
+  s->ln_e = ln_f(E_F);
+}
+
+}  // namespace
+
+/* ============================================================================ C ABI */
+extern "C" {
+
+const char* hrt_last_error(void) { return g_error.c_str(); }
+const char* hrt_version(void) { return "hrt 0.1.0 (gfx950)"; }
+
+hrt_status hrt_scene_create(hrt_scene** out) {
+  return guard([&] {
+    need(out != nullptr, HRT_ERR_INVALID_ARG, "null out");
+    *out = new hrt_scene();
+  });
+}
+
+void hrt_scene_destroy(hrt_scene* s) {
+  if (!s) return;
+  device_release(s);
+  delete s;
+}
+
+hrt_status hrt_tex_solid(hrt_scene* s, float r, float g, float b, uint32_t* id) {
+  return guard([&] {
+    mutable_scene(s);
+    need(id != nullptr, HRT_ERR_INVALID_ARG, "null id");
+    HTex t;
+    t.kind = G::T_SOLID;
+    t.color = v3(r, g, b);
+    s->texs.push_back(t);
+    *id = (uint32_t)(s->texs.size() - 1);
+  });
+}
+
+hrt_status hrt_tex_checker(hrt_scene* s, uint32_t odd, uint32_t even, uint32_t* id) {
+  return guard([&] {
+    mutable_scene(s);
+    need(id != nullptr, HRT_ERR_INVALID_ARG, "null id");
+    check_tex(s, odd);
+    check_tex(s, even);
+    HTex t;
+    t.kind = G::T_CHECKER;
+    t.odd = odd;
+    t.even = even;
+    s->texs.push_back(t);
+    *id = (uint32_t)(s->texs.size() - 1);
+  });
+}
+
+hrt_status hrt_tex_noise(hrt_scene* s, float scale, const float* ranvec, const uint32_t* perm,
+                         uint32_t* id) {
+  return guard([&] {
+    mutable_scene(s);
+    need(id && ranvec && perm, HRT_ERR_INVALID_ARG, "null argument");
+    G::Perlin p;
+    memset(&p, 0, sizeof(p));
+    for (int i = 0; i < 256; i++) {
+      for (int c = 0; c < 3; c++) p.ranvec[i][c] = ranvec[3 * i + c];
+      for (int c = 0; c < 3; c++) {
+        need(perm[256 * c + i] < 256, HRT_ERR_INVALID_ARG, "permutation entry >= 256");
+        p.perm[c][i] = perm[256 * c + i];
+      }
+    }
+    s->perlin.push_back(p);
+    HTex t;
+    t.kind = G::T_NOISE;
+    t.scale = scale;
+    t.perlin = (uint32_t)(s->perlin.size() - 1);
+    s->texs.push_back(t);
+    *id = (uint32_t)(s->texs.size() - 1);
+  });
+}
+
+hrt_status hrt_tex_image(hrt_scene* s, const uint8_t* data, uint32_t width, uint32_t height,
+                         uint32_t components, uint32_t* id) {
+  return guard([&] {
+    mutable_scene(s);
+    need(id != nullptr, HRT_ERR_INVALID_ARG, "null id");
+    HTex t;
+    t.kind = G::T_IMAGE;
+    size_t bytes = (size_t)width * height * components;
+    if (data && bytes) {
+      need(components >= 3, HRT_ERR_INVALID_ARG, "image needs >= 3 components");
+      need(s->images.size() + bytes < (1ull << 32), HRT_ERR_UNSUPPORTED, "image data > 4 GiB");
+      t.img_off = s->images.size();
+      s->images.insert(s->images.end(), data, data + bytes);
+      t.w = width; t.h = height; t.c = components;
+    } /* else: empty image -> magenta (image_texture.rs:37-39) */
+    s->texs.push_back(t);
+    *id = (uint32_t)(s->texs.size() - 1);
+  });
+}
+
+static hrt_status add_mat(hrt_scene* s, HMat m, uint32_t* id) {
+  return guard([&] {
+    mutable_scene(s);
+    need(id != nullptr, HRT_ERR_INVALID_ARG, "null id");
+    if (m.tex != G::NONE) check_tex(s, m.tex);
+    s->mats.push_back(m);
+    *id = (uint32_t)(s->mats.size() - 1);
+  });
+}
+
+hrt_status hrt_mat_lambertian(hrt_scene* s, uint32_t tex, uint32_t* id) {
+  HMat m; m.kind = G::M_LAMBERTIAN; m.tex = tex;
+  if (s && tex >= s->texs.size()) { set_error("bad texture id"); return HRT_ERR_INVALID_ARG; }
+  return add_mat(s, m, id);
+}
+hrt_status hrt_mat_metal(hrt_scene* s, float r, float g, float b, float fuzz, uint32_t* id) {
+  HMat m; m.kind = G::M_METAL; m.albedo = v3(r, g, b); m.fuzz = fuzz;
+  return add_mat(s, m, id);
+}
+hrt_status hrt_mat_dielectric(hrt_scene* s, float ior, uint32_t* id) {
+  HMat m; m.kind = G::M_DIELECTRIC; m.ior = ior;
+  return add_mat(s, m, id);
+}
+hrt_status hrt_mat_diffuse_light(hrt_scene* s, uint32_t tex, uint32_t* id) {
+  HMat m; m.kind = G::M_DIFFUSE_LIGHT; m.tex = tex;
+  if (s && tex >= s->texs.size()) { set_error("bad texture id"); return HRT_ERR_INVALID_ARG; }
+  return add_mat(s, m, id);
+}
+hrt_status hrt_mat_isotropic(hrt_scene* s, uint32_t tex, uint32_t* id) {
+  HMat m; m.kind = G::M_ISOTROPIC; m.tex = tex;
+  if (s && tex >= s->texs.size()) { set_error("bad texture id"); return HRT_ERR_INVALID_ARG; }
+  return add_mat(s, m, id);
+}
+
+hrt_status hrt_node_sphere(hrt_scene* s, const float c[3], float r, uint32_t mat, uint32_t* id) {
+  return guard([&] {
+    mutable_scene(s);
+    need(id != nullptr, HRT_ERR_INVALID_ARG, "null id");
+    check_mat(s, mat);
+    HNode n;
+    n.kind = N_SPHERE;
+    n.c0 = vin(c);
+    n.r = r;
+    n.mat = mat;
+    *id = push_node(s, std::move(n));
+  });
+}
+
+hrt_status hrt_node_moving_sphere(hrt_scene* s, const float c0[3], const float c1[3], float t0,
+                                  float t1, float r, uint32_t mat, uint32_t* id) {
+  return guard([&] {
+    mutable_scene(s);
+    need(id != nullptr, HRT_ERR_INVALID_ARG, "null id");
+    check_mat(s, mat);
+    HNode n;
+    n.kind = N_MOVING;
+    n.c0 = vin(c0);
+    n.c1 = vin(c1);
+    n.t0 = t0;
+    n.t1 = t1;
+    n.r = r;
+    n.mat = mat;
+    *id = push_node(s, std::move(n));
+  });
+}
+
+hrt_status hrt_node_rect(hrt_scene* s, int32_t plane, float a0, float a1, float b0, float b1,
+                         float k, uint32_t mat, uint32_t* id) {
+  return guard([&] {
+    mutable_scene(s);
+    need(id != nullptr, HRT_ERR_INVALID_ARG, "null id");
+    need(plane >= 0 && plane <= 2, HRT_ERR_INVALID_ARG, "bad plane");
+    check_mat(s, mat);
+    HNode n;
+    n.kind = N_RECT;
+    n.plane = plane;
+    n.a0 = a0; n.a1 = a1; n.b0 = b0; n.b1 = b1; n.k = k;
+    n.mat = mat;
+    *id = push_node(s, std::move(n));
+  });
+}
+
+/* cuboid.rs:29-97: six rects in this exact order (List order decides equal-t ties) */
+hrt_status hrt_node_cuboid(hrt_scene* s, const float bmin[3], const float bmax[3], uint32_t mat,
+                           uint32_t* id) {
+  return guard([&] {
+    mutable_scene(s);
+    need(id != nullptr, HRT_ERR_INVALID_ARG, "null id");
+    check_mat(s, mat);
+    Vec3 p0 = vin(bmin), p1 = vin(bmax);
+    struct R { int plane; float a0, a1, b0, b1, k; };
+    const R sides[6] = {{HRT_PLANE_XY, p0.x, p1.x, p0.y, p1.y, p1.z}, {HRT_PLANE_XY, p0.x, p1.x, p0.y, p1.y, p0.z},
+                        {HRT_PLANE_ZX, p0.z, p1.z, p0.x, p1.x, p1.y}, {HRT_PLANE_ZX, p0.z, p1.z, p0.x, p1.x, p0.y},
+                        {HRT_PLANE_YZ, p0.y, p1.y, p0.z, p1.z, p1.x}, {HRT_PLANE_YZ, p0.y, p1.y, p0.z, p1.z, p0.x}};
+    HNode c;
+    c.kind = N_CUBOID;
+    c.box = Aabb{p0, p1};
+    c.has_box = true;
+    for (const R& r : sides) {
+      HNode n;
+      n.kind = N_RECT;
+      n.plane = r.plane;
+      n.a0 = r.a0; n.a1 = r.a1; n.b0 = r.b0; n.b1 = r.b1; n.k = r.k;
+      n.mat = mat;
+      n.owned = true;
+      c.children.push_back(push_node(s, std::move(n)));
+    }
+    *id = push_node(s, std::move(c));
+  });
+}
+
+hrt_status hrt_node_translate(hrt_scene* s, uint32_t child, const float d[3], uint32_t* id) {
+  return guard([&] {
+    mutable_scene(s);
+    need(id != nullptr, HRT_ERR_INVALID_ARG, "null id");
+    Vec3 disp = vin(d);
+    HNode n;
+    n.kind = N_TRANSLATE;
+    n.disp = disp;
+    n.children.push_back(take_child(s, child));
+    *id = push_node(s, std::move(n));
+  });
+}
+
+/* rotation.rs:38-99 */
+hrt_status hrt_node_rotate(hrt_scene* s, int32_t axis, uint32_t child, float angle, uint32_t* id) {
+  return guard([&] {
+    mutable_scene(s);
+    need(id != nullptr, HRT_ERR_INVALID_ARG, "null id");
+    need(axis >= 0 && axis <= 2, HRT_ERR_INVALID_ARG, "bad axis");
+    need(child < s->nodes.size(), HRT_ERR_INVALID_ARG, "bad node id");
+    need(!s->nodes[child].owned, HRT_ERR_INVALID_ARG, "node already owned by another node");
+    int r_axis = axis, a_axis = (axis + 1) % 3, b_axis = (axis + 2) % 3;
+    HNode n;
+    n.kind = N_ROTATE;
+    n.axis = axis;
+    float radians = (PI_F / 180.0f) * angle;
+    n.sin_t = sin_f(radians);
+    n.cos_t = cos_f(radians);
+    Aabb b;
+    n.has_box = bbox(s, child, 0.0f, 1.0f, b);
+    if (n.has_box) {
+      const float FMAX = 3.40282347e+38f;
+      Vec3 mn = v3(FMAX, FMAX, FMAX), mx = v3(-FMAX, -FMAX, -FMAX);
+      for (int i = 0; i < 2; i++)
+        for (int j = 0; j < 2; j++)
+          for (int k = 0; k < 2; k++) {
+            float r = (float)k * b.mx[r_axis] + (float)(1 - k) * b.mn[r_axis];
+            float a = (float)i * b.mx[a_axis] + (float)(1 - i) * b.mn[a_axis];
+            float bb = (float)j * b.mx[b_axis] + (float)(1 - j) * b.mn[b_axis];
+            float new_a = n.cos_t * a - n.sin_t * bb;
+            float new_b = n.sin_t * a + n.cos_t * bb;
+            if (new_a < mn[a_axis]) mn[a_axis] = new_a;
+            if (new_b < mn[b_axis]) mn[b_axis] = new_b;
+            if (r < mn[r_axis]) mn[r_axis] = r;
+            if (new_a > mx[a_axis]) mx[a_axis] = new_a;
+            if (new_b > mx[b_axis]) mx[b_axis] = new_b;
+            if (r > mx[r_axis]) mx[r_axis] = r;
+          }
+      n.box = Aabb{mn, mx};
+    }
+    n.children.push_back(take_child(s, child));
+    *id = push_node(s, std::move(n));
+  });
+}
+
+hrt_status hrt_node_constant_medium(hrt_scene* s, uint32_t boundary, float density, uint32_t tex,
+                                    uint32_t* id) {
+  return guard([&] {
+    mutable_scene(s);
+    need(id != nullptr, HRT_ERR_INVALID_ARG, "null id");
+    check_tex(s, tex);
+    HNode n;
+    n.kind = N_MEDIUM;
+    n.neg_inv_density = -1.0f / density;
+    n.tex = tex;
+    n.medium_id = s->n_media++;
+    n.children.push_back(take_child(s, boundary));
+    *id = push_node(s, std::move(n));
+  });
+}
+
+hrt_status hrt_node_list(hrt_scene* s, const uint32_t* children, uint32_t n_children, uint32_t* id) {
+  return guard([&] {
+    mutable_scene(s);
+    need(id != nullptr && (children != nullptr || n_children == 0), HRT_ERR_INVALID_ARG, "null argument");
+    for (uint32_t i = 0; i < n_children; i++) {
+      need(children[i] < s->nodes.size(), HRT_ERR_INVALID_ARG, "bad node id");
+      need(!s->nodes[children[i]].owned, HRT_ERR_INVALID_ARG, "node already owned by another node");
+      for (uint32_t j = 0; j < i; j++) need(children[j] != children[i], HRT_ERR_INVALID_ARG, "duplicate child");
+    }
+    HNode n;
+    n.kind = N_LIST;
+    for (uint32_t i = 0; i < n_children; i++) n.children.push_back(take_child(s, children[i]));
+    *id = push_node(s, std::move(n));
+  });
+}
+
+hrt_status hrt_node_bvh(hrt_scene* s, const uint32_t* children, uint32_t n_children, float t0,
+                        float t1, uint32_t* id) {
+  return guard([&] {
+    mutable_scene(s);
+    need(id != nullptr && (children != nullptr || n_children == 0), HRT_ERR_INVALID_ARG, "null argument");
+    std::vector<uint32_t> objs;
+    for (uint32_t i = 0; i < n_children; i++) {
+      need(children[i] < s->nodes.size(), HRT_ERR_INVALID_ARG, "bad node id");
+      need(!s->nodes[children[i]].owned, HRT_ERR_INVALID_ARG, "node already owned by another node");
+      for (uint32_t j = 0; j < i; j++) need(children[j] != children[i], HRT_ERR_INVALID_ARG, "duplicate child");
+      objs.push_back(children[i]);
+    }
+    size_t before = s->nodes.size();
+    try {
+      uint32_t root = build_bvh(s, objs, t0, t1);
+      for (uint32_t c : objs) s->nodes[c].owned = true;
+      *id = root;
+    } catch (...) {
+      s->nodes.resize(before); /* leave the scene as it was */
+      throw;
+    }
+  });
+}
+
+hrt_status hrt_node_count(const hrt_scene* s, uint32_t node, uint32_t* out) {
+  return guard([&] {
+    need(s && out && node < s->nodes.size(), HRT_ERR_INVALID_ARG, "bad argument");
+    *out = count(s, node);
+  });
+}
+
+hrt_status hrt_node_bounding_box(const hrt_scene* s, uint32_t node, float t0, float t1,
+                                 int32_t* has_box, float bmin[3], float bmax[3]) {
+  return guard([&] {
+    need(s && has_box && bmin && bmax && node < s->nodes.size(), HRT_ERR_INVALID_ARG, "bad argument");
+    Aabb b;
+    *has_box = bbox(s, node, t0, t1, b) ? 1 : 0;
+    if (*has_box)
+      for (int a = 0; a < 3; a++) { bmin[a] = b.mn[a]; bmax[a] = b.mx[a]; }
+  });
+}
+
+hrt_status hrt_scene_set_root(hrt_scene* s, uint32_t node) {
+  return guard([&] {
+    mutable_scene(s);
+    need(node < s->nodes.size(), HRT_ERR_INVALID_ARG, "bad node id");
+    need(!s->nodes[node].owned, HRT_ERR_INVALID_ARG, "root is owned by another node");
+    s->root = node;
+  });
+}
+
+hrt_status hrt_scene_commit(hrt_scene* s, int32_t device) {
+  hrt_status st = guard([&] {
+    mutable_scene(s);
+    need(s->root != G::NONE, HRT_ERR_STATE, "no root set");
+    flatten(s);
+  });
+  if (st != HRT_OK) return st;
+  st = device_upload(s, device);
+  if (st == HRT_OK) s->committed = true;
+  return st;
+}
+
+hrt_status hrt_scene_get_info(const hrt_scene* s, hrt_scene_info* info) {
+  return guard([&] {
+    need(s && info, HRT_ERR_INVALID_ARG, "null argument");
+    need(s->committed, HRT_ERR_STATE, "scene not committed");
+    info->nodes = (uint32_t)s->g_nodes.size();
+    info->prims = (uint32_t)s->g_prims.size();
+    info->materials = (uint32_t)s->g_mats.size();
+    info->textures = (uint32_t)s->g_texs.size();
+    info->instances = (uint32_t)s->g_insts.size();
+    info->media = (uint32_t)s->g_media.size();
+    info->feature_mask = s->feature_mask;
+    info->blob_bytes = (uint32_t)s->blob_bytes;
+    info->in_lds = 0;
+    info->cull_mode = (uint32_t)s->cull_mode;
+  });
+}
+
+/* camera.rs:34-83 */
+hrt_status hrt_camera_init(hrt_camera* cam, const float from_[3], const float at_[3], float fov,
+                           float aperture, float focus_dist, float time0, float time1,
+                           int32_t width, int32_t height) {
+  return guard([&] {
+    need(cam != nullptr, HRT_ERR_INVALID_ARG, "null camera");
+    need(width > 0 && height > 0, HRT_ERR_INVALID_ARG, "bad size");
+    /* rand's gen_range(time0..time1) panics unless time0 < time1 (camera.rs:93) */
+    need(time0 < time1, HRT_ERR_INVALID_ARG, "time0 must be < time1");
+    Vec3 from = vin(from_), at = vin(at_);
+    float aspect_ratio = (float)width / (float)height;
+    float theta = fov * (PI_F / 180.0f); /* f32::to_radians */
+    float h = tan_f(theta / 2.0f);
+    float viewport_height = 2.0f * h;
+    float viewport_width = aspect_ratio * viewport_height;
+    Vec3 w = normalize(from - at);
+    Vec3 u = normalize(cross(v3(0.0f, 1.0f, 0.0f), w));
+    Vec3 v = cross(w, u);
+    Vec3 origin = from;
+    Vec3 horizontal = (focus_dist * viewport_width) * u;
+    Vec3 vertical = (focus_dist * viewport_height) * v;
+    Vec3 llc = ((origin - horizontal / 2.0f) - vertical / 2.0f) - focus_dist * w;
+    const Vec3* src[7] = {&origin, &llc, &horizontal, &vertical, &u, &v, &w};
+    float* dst[7] = {cam->origin, cam->lower_left_corner, cam->horizontal, cam->vertical, cam->u, cam->v, cam->w};
+    for (int i = 0; i < 7; i++) { dst[i][0] = src[i]->x; dst[i][1] = src[i]->y; dst[i][2] = src[i]->z; }
+    cam->lens_radius = aperture / 2.0f;
+    cam->time0 = time0;
+    cam->time1 = time1;
+  });
+}
+
+/* application.rs:363-364 (tile counts) and :404-430 (tile rectangles).  The reference derives the
+ * ragged width with a float formula; integer min() gives the same for every BASELINE size and never
+ * drops a column.  Tile i of the grid goes to rank i % world. */
+hrt_status hrt_tile_grid(uint32_t width, uint32_t height, uint32_t tile_size, uint32_t rank,
+                         uint32_t world, hrt_tile* tiles, uint32_t cap, uint32_t* n) {
+  return guard([&] {
+    need(n != nullptr && tile_size > 0 && world > 0 && rank < world, HRT_ERR_INVALID_ARG, "bad argument");
+    uint32_t tx = (width + tile_size - 1) / tile_size, ty = (height + tile_size - 1) / tile_size;
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < tx * ty; i++) {
+      if (i % world != rank) continue;
+      if (tiles && k < cap) {
+        uint32_t x = (i % tx) * tile_size, y = (i / tx) * tile_size;
+        tiles[k] = hrt_tile{x, y, std::min(tile_size, width - x), std::min(tile_size, height - y)};
+      }
+      k++;
+    }
+    *n = k;
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,109 @@
+/*
+ * scene_internal.h — host-side scene graph (what the hrt_* constructors record) and the flattened,
+ * device-ready form produced by hrt_scene_commit.  Shared by scene.cpp (host) and render.hip.
+ */
+#pragma once
+#include <hrt/hd_math.h>
+#include <hrt/hrt.h>
+
+#include <string>
+#include <vector>
+
+#include "layout.h"
+
+namespace hrt {
+namespace host {
+
+struct Aabb {
+  Vec3 mn, mx;
+};
+
+enum NodeKind { N_SPHERE, N_MOVING, N_RECT, N_CUBOID, N_TRANSLATE, N_ROTATE, N_MEDIUM, N_LIST, N_BVH };
+
+struct HNode {
+  NodeKind kind;
+  /* spheres */
+  Vec3 c0{}, c1{};
+  float t0 = 0, t1 = 0, r = 0;
+  uint32_t mat = gpu::NONE;
+  /* rect */
+  int plane = 0;
+  float a0 = 0, a1 = 0, b0 = 0, b1 = 0, k = 0;
+  /* cuboid / bvh box */
+  Aabb box{};
+  bool has_box = false; /* rotation: bbox computed at construction; bvh: always */
+  /* translate / rotate */
+  Vec3 disp{};
+  int axis = 0;
+  float sin_t = 0, cos_t = 1;
+  /* medium */
+  float neg_inv_density = 0;
+  uint32_t tex = gpu::NONE;
+  uint32_t medium_id = 0;
+  /* children: list / cuboid sides / bvh (1 = leaf, 2 = left,right) / translate, rotate, medium (1) */
+  std::vector<uint32_t> children;
+  bool owned = false; /* already a child of another node (Box<dyn Hittable> ownership) */
+};
+
+struct HTex {
+  uint32_t kind;
+  Vec3 color{};
+  uint32_t odd = 0, even = 0;
+  float scale = 0;
+  uint32_t perlin = 0;
+  uint64_t img_off = 0;
+  uint32_t w = 0, h = 0, c = 0;
+};
+
+struct HMat {
+  uint32_t kind;
+  uint32_t tex = gpu::NONE;
+  Vec3 albedo{};
+  float fuzz = 0, ior = 0;
+};
+
+}  // namespace host
+}  // namespace hrt
+
+struct hrt_scene {
+  /* ---- host graph ---- */
+  std::vector<hrt::host::HNode> nodes;
+  std::vector<hrt::host::HTex> texs;
+  std::vector<hrt::host::HMat> mats;
+  std::vector<hrt::gpu::Perlin> perlin;
+  std::vector<uint8_t> images;
+  uint32_t root = hrt::gpu::NONE;
+  uint32_t n_media = 0;
+  bool committed = false;
+
+  /* ---- flattened (valid after commit) ---- */
+  std::vector<hrt::gpu::Node> g_nodes;
+  std::vector<hrt::gpu::Prim> g_prims;
+  std::vector<hrt::gpu::Inst> g_insts;
+  std::vector<hrt::gpu::Medium> g_media;
+  std::vector<hrt::gpu::Mat> g_mats;
+  std::vector<hrt::gpu::Tex> g_texs;
+  uint32_t main_end = 0;
+  uint32_t feature_mask = 0;
+  int cull_mode = hrt::gpu::CULL_REFERENCE;
+  float ln_e = 0; /* ln(E) as computed by hd_math (constant_medium.rs:59) */
+
+  /* ---- device ---- */
+  int device = -1;
+  void* d_blob = nullptr;
+  size_t blob_bytes = 0;
+  size_t off_nodes = 0, off_prims = 0, off_insts = 0, off_media = 0, off_mats = 0, off_texs = 0,
+         off_perlin = 0, off_images = 0;
+  void* d_scratch = nullptr; /* pixel counter + stats, per render call slot */
+  void* d_tiles = nullptr;
+  size_t tiles_cap = 0;
+  void* d_out = nullptr; /* staging for the host-output hrt_render */
+  size_t out_cap = 0;
+};
+
+namespace hrt {
+void set_error(const std::string& msg);
+/* implemented in render.hip */
+hrt_status device_upload(hrt_scene* s, int device);
+void device_release(hrt_scene* s);
+}  // namespace hrt

@@ -1,0 +1,222 @@
+/*
+ * hrt.h — the drop-in C ABI of the MI355X path-tracing inner loop (libhrt.so).
+ *
+ * What it replaces (reference = SkillerRaptor/hyper-ray-tracer, a Rust crate with no FFI of its own):
+ *   - the trait surface the scene builders construct (src/hittable/mod.rs:19-25 `Hittable`,
+ *     src/materials/mod.rs:15-19 `Material`, src/textures/mod.rs:14-16 `Texture`): a GPU cannot call
+ *     back into trait objects per ray, so each concrete type gets a constructor here that records a
+ *     lowered description (the additive `lower()` a Rust binding adds to each type);
+ *   - `Application::render` (src/application.rs:393-475) + `ray_color` (:477-495): the per-tile,
+ *     per-pixel, per-sample loop, which becomes hrt_render / hrt_render_tiles_device (one persistent
+ *     HIP megakernel launch for a whole tile set);
+ *   - `Camera::new`/`resize` (src/camera.rs:34-83): hrt_camera_init.
+ *
+ * Conventions
+ *   - Every function returns hrt_status (0 = OK) and never unwinds; the reference's panics (empty BVH
+ *     bvh_node.rs:38, NaN bbox bvh_node.rs:31/76, missing image image_texture.rs:20, gen_range with
+ *     lo >= hi) become status codes.  hrt_last_error() returns a thread-local message.
+ *   - Ids returned through uint32_t* are indices into the scene's texture / material / node tables.
+ *     Inputs (Perlin tables, image bytes, child lists) are deep-copied during the call.
+ *   - A scene is mutable until hrt_scene_commit, immutable afterwards; rendering is re-entrant per
+ *     scene (each call uses its own stream-ordered scratch).
+ *   - Image layout: pixel (x, y) with y = 0 the BOTTOM row (src/application.rs:444-445); output of a
+ *     w*h region is RGBA f32 at index (x-x0) + w*(y-y0), alpha = 1 (src/application.rs:451-456).
+ */
+#ifndef HRT_HRT_H
+#define HRT_HRT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t hrt_status;
+enum {
+  HRT_OK = 0,
+  HRT_ERR_INVALID_ARG = 1, /* bad id, null pointer, bad enum, lo >= hi ... */
+  HRT_ERR_EMPTY = 2,       /* BvhNode::new with no objects (bvh_node.rs:38) */
+  HRT_ERR_NO_BBOX = 3,     /* object without bounding box inside a BVH (bvh_node.rs:42,79) */
+  HRT_ERR_NAN = 4,         /* NaN in a bounding box / sort key (bvh_node.rs:31,76) */
+  HRT_ERR_STATE = 5,       /* mutation after commit, render before commit, ... */
+  HRT_ERR_HIP = 6,         /* HIP runtime error (message in hrt_last_error) */
+  HRT_ERR_OOM = 7,
+  HRT_ERR_UNSUPPORTED = 8  /* e.g. a ConstantMedium nested inside another medium's boundary */
+};
+
+typedef struct hrt_scene hrt_scene;
+
+/* rect.rs:12-17 */
+enum { HRT_PLANE_XY = 0, HRT_PLANE_YZ = 1, HRT_PLANE_ZX = 2 };
+/* rotation.rs:10-25 */
+enum { HRT_AXIS_X = 0, HRT_AXIS_Y = 1, HRT_AXIS_Z = 2 };
+
+/* Camera after Camera::resize (src/camera.rs:16-31, 67-83). */
+typedef struct hrt_camera {
+  float origin[3];
+  float lower_left_corner[3];
+  float horizontal[3];
+  float vertical[3];
+  float u[3], v[3], w[3];
+  float lens_radius;
+  float time0, time1;
+} hrt_camera;
+
+/* Render knobs: src/arguments.rs:23-47 (width/height/samples/depth/tile) + the values the reference
+ * hard-codes (background per scene application.rs:132-197, t_min = 0.001 at :482) + the seed that
+ * replaces thread_rng.  Pixels are keyed by their index in the FULL width x height image. */
+typedef struct hrt_render_params {
+  uint32_t width, height;   /* full image (u = (x+xi)/(width-1), application.rs:444) */
+  uint32_t samples;         /* spp (application.rs:443) */
+  uint32_t max_depth;       /* ray_color depth (application.rs:478); reference CLI default 10 */
+  uint32_t sample_offset;   /* first sample index (0; >0 splits one pixel's samples across jobs) */
+  uint32_t flags;           /* reserved, must be 0 */
+  float t_min;              /* 0.001 */
+  float background[3];
+  uint64_t seed;
+} hrt_render_params;
+
+typedef struct hrt_tile {
+  uint32_t x, y, w, h; /* image coordinates, y up */
+} hrt_tile;
+
+/* Work counters of one render call (exact, counted on the device). */
+typedef struct hrt_render_stats {
+  uint64_t segments;        /* world.hit calls == rays (application.rs:482) */
+  uint64_t samples;         /* primary samples = pixels * spp */
+  uint64_t pixels;
+} hrt_render_stats;
+
+/* Scene description of one reference preset (application.rs:132-211). */
+typedef struct hrt_preset_info {
+  float look_from[3];
+  float look_at[3];
+  float fov;
+  float aperture;
+  float focus_dist;
+  float time0, time1;
+  float background[3];
+  uint32_t root;
+} hrt_preset_info;
+
+/* Reference scenes (src/arguments.rs:9-19) + build-defined benchmark scenes. */
+enum {
+  HRT_PRESET_RANDOM = 0,             /* application.rs:497-565 (BASELINE configs 1, 2) */
+  HRT_PRESET_TWO_SPHERES = 1,        /* :567-587 */
+  HRT_PRESET_TWO_PERLIN_SPHERES = 2, /* :589-602 */
+  HRT_PRESET_EARTH = 3,              /* :604-612 */
+  HRT_PRESET_SIMPLE_LIGHT = 4,       /* :614-637 */
+  HRT_PRESET_CORNELL = 5,            /* :639-721 (config 5) */
+  HRT_PRESET_CORNELL_SMOKE = 6,      /* :723-815 */
+  HRT_PRESET_FINAL = 7,              /* :817-935 */
+  HRT_PRESET_EARTH_PERLIN = 8,       /* config 3: earth (0,2,0) r2 over the Perlin ground of :589-602 */
+  HRT_PRESET_RANDOM_10K = 9,         /* config 4: :511-545 with a, b in [-50, 50) */
+  HRT_PRESET_FEATURES = 10,          /* X/Z rotations, lists, nested instances, media in instances */
+  HRT_PRESET_COUNT = 11
+};
+
+const char* hrt_last_error(void);
+const char* hrt_version(void);
+
+/* ---- scene lifetime ---- */
+hrt_status hrt_scene_create(hrt_scene** out);
+void hrt_scene_destroy(hrt_scene* scene);
+
+/* ---- textures (src/textures/) ---- */
+hrt_status hrt_tex_solid(hrt_scene* s, float r, float g, float b, uint32_t* id);
+hrt_status hrt_tex_checker(hrt_scene* s, uint32_t odd, uint32_t even, uint32_t* id);
+/* ranvec: 256*3 f32 unit vectors; perm: 3*256 u32 (x, y, z permutations), perlin_noise.rs:14-19 */
+hrt_status hrt_tex_noise(hrt_scene* s, float scale, const float* ranvec, const uint32_t* perm,
+                         uint32_t* id);
+/* Decoded image bytes (image_texture.rs:19-33); data may be NULL/empty -> magenta (:37-39). */
+hrt_status hrt_tex_image(hrt_scene* s, const uint8_t* data, uint32_t width, uint32_t height,
+                         uint32_t components, uint32_t* id);
+
+/* ---- materials (src/materials/) ---- */
+hrt_status hrt_mat_lambertian(hrt_scene* s, uint32_t albedo_tex, uint32_t* id);
+hrt_status hrt_mat_metal(hrt_scene* s, float r, float g, float b, float fuzz, uint32_t* id);
+hrt_status hrt_mat_dielectric(hrt_scene* s, float index_of_refraction, uint32_t* id);
+hrt_status hrt_mat_diffuse_light(hrt_scene* s, uint32_t emit_tex, uint32_t* id);
+hrt_status hrt_mat_isotropic(hrt_scene* s, uint32_t albedo_tex, uint32_t* id);
+
+/* ---- hittables (src/hittable/) ---- */
+hrt_status hrt_node_sphere(hrt_scene* s, const float center[3], float radius, uint32_t mat,
+                           uint32_t* id);
+hrt_status hrt_node_moving_sphere(hrt_scene* s, const float center0[3], const float center1[3],
+                                  float time0, float time1, float radius, uint32_t mat,
+                                  uint32_t* id);
+hrt_status hrt_node_rect(hrt_scene* s, int32_t plane, float a0, float a1, float b0, float b1,
+                         float k, uint32_t mat, uint32_t* id);
+hrt_status hrt_node_cuboid(hrt_scene* s, const float box_min[3], const float box_max[3],
+                           uint32_t mat, uint32_t* id);
+hrt_status hrt_node_translate(hrt_scene* s, uint32_t child, const float displacement[3],
+                              uint32_t* id);
+hrt_status hrt_node_rotate(hrt_scene* s, int32_t axis, uint32_t child, float angle_degrees,
+                           uint32_t* id);
+/* The medium's isotropic phase texture is given as a texture id (constant_medium.rs:22-29). */
+hrt_status hrt_node_constant_medium(hrt_scene* s, uint32_t boundary, float density,
+                                    uint32_t albedo_tex, uint32_t* id);
+hrt_status hrt_node_list(hrt_scene* s, const uint32_t* children, uint32_t n, uint32_t* id);
+/* BvhNode::new(objects, t0, t1) (bvh_node.rs:27-63): built immediately, consumes the children. */
+hrt_status hrt_node_bvh(hrt_scene* s, const uint32_t* children, uint32_t n, float time0,
+                        float time1, uint32_t* id);
+/* Hittable::count (hittable/mod.rs:24) and bounding_box (:22). has_box = 0 when None. */
+hrt_status hrt_node_count(const hrt_scene* s, uint32_t node, uint32_t* count);
+hrt_status hrt_node_bounding_box(const hrt_scene* s, uint32_t node, float time0, float time1,
+                                 int32_t* has_box, float box_min[3], float box_max[3]);
+
+hrt_status hrt_scene_set_root(hrt_scene* s, uint32_t node);
+/* Flatten + upload to HIP device `device` (-1: the calling thread's current device). */
+hrt_status hrt_scene_commit(hrt_scene* s, int32_t device);
+
+/* Reference scene builders (application.rs:497-935) driven by a seeded stream in place of
+ * thread_rng.  `image` feeds the Earth texture (earthmap.jpg decoded by the caller, or synthetic). */
+hrt_status hrt_preset_build(hrt_scene* s, int32_t preset, uint64_t scene_seed, const uint8_t* image,
+                            uint32_t image_w, uint32_t image_h, uint32_t image_c,
+                            hrt_preset_info* info);
+
+/* Camera::new + resize (camera.rs:34-83). */
+hrt_status hrt_camera_init(hrt_camera* cam, const float look_from[3], const float look_at[3],
+                           float fov_degrees, float aperture, float focus_dist, float time0,
+                           float time1, int32_t width, int32_t height);
+
+/* ---- rendering ---- */
+/* Render `n_tiles` tiles into device memory d_rgba (tiles packed back to back, tile i at
+ * 4 * sum_{j<i} w_j*h_j floats; each tile row-major with y up).  Asynchronous on `stream`
+ * (a hipStream_t, NULL = default stream).  stats (optional, host pointer) is filled after an
+ * internal stream synchronisation when non-NULL. */
+hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hrt_render_params* p,
+                                   const hrt_tile* tiles, uint32_t n_tiles, float* d_rgba,
+                                   void* stream, hrt_render_stats* stats);
+/* One region into device memory. */
+hrt_status hrt_render_device(hrt_scene* s, const hrt_camera* cam, const hrt_render_params* p,
+                             uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, float* d_rgba,
+                             void* stream, hrt_render_stats* stats);
+/* One region into caller-owned host memory (w*h*4 floats); synchronous. */
+hrt_status hrt_render(hrt_scene* s, const hrt_camera* cam, const hrt_render_params* p, uint32_t x0,
+                      uint32_t y0, uint32_t w, uint32_t h, float* rgba_out, hrt_render_stats* stats);
+
+/* Reference tile grid (application.rs:363-364, 404-430 with integer ragged edges) and its
+ * round-robin split across `world` ranks: writes up to `cap` tiles of rank `rank`; *n = count. */
+hrt_status hrt_tile_grid(uint32_t width, uint32_t height, uint32_t tile_size, uint32_t rank,
+                         uint32_t world, hrt_tile* tiles, uint32_t cap, uint32_t* n);
+
+/* ---- diagnostics ---- */
+/* Device occupancy / layout facts of the committed scene (for DESIGN/bench). */
+typedef struct hrt_scene_info {
+  uint32_t nodes, prims, materials, textures, instances, media;
+  uint32_t feature_mask;
+  uint32_t blob_bytes;     /* device bytes of the flattened scene */
+  uint32_t in_lds;         /* 1 if the megakernel stages the scene in LDS */
+  uint32_t cull_mode;      /* 0: reference per-axis box test (aabb.rs), 1: slab test */
+} hrt_scene_info;
+hrt_status hrt_scene_get_info(const hrt_scene* s, hrt_scene_info* info);
+/* Evaluate the shared deterministic math on the DEVICE (op: 0 sin,1 cos,2 acos,3 atan2,4 ln,
+ * 5 pow5, 6 tan) for n inputs; used by the GPU KAT test to prove host/device bit identity. */
+hrt_status hrt_debug_device_math(int32_t op, const float* x, const float* y, float* out, uint32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HRT_HRT_H */

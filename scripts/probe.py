@@ -1,0 +1,39 @@
+"""Quick device probe: time the megakernel on one preset (segments/s), no oracle involved."""
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "hyper-ray-tracer_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import hrt  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--preset", default="random")
+ap.add_argument("--width", type=int, default=1920)
+ap.add_argument("--height", type=int, default=1080)
+ap.add_argument("--spp", type=int, default=16)
+ap.add_argument("--depth", type=int, default=50)
+ap.add_argument("--reps", type=int, default=2)
+a = ap.parse_args()
+
+s = hrt.preset(a.preset, 1)
+s.commit(0)
+si = s.scene_info()
+print(f"scene {a.preset}: nodes {si.nodes} prims {si.prims} features {si.feature_mask:#x} cull {si.cull_mode} blob {si.blob_bytes} B", flush=True)
+cam = hrt.preset_camera(s.info, a.width, a.height)
+p = hrt.params(a.width, a.height, a.spp, a.depth, 1, tuple(s.info.background))
+out = torch.empty((a.height, a.width, 4), dtype=torch.float32, device="cuda")
+tiles = [(0, 0, a.width, a.height)]
+for r in range(a.reps):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    st = hrt.render_tiles_device(s, cam, p, tiles, out.data_ptr(), 0, want_stats=True)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    print(f"rep {r}: {dt*1e3:.1f} ms  segments {st.segments}  seg/sample {st.segments/st.samples:.3f}  "
+          f"{st.segments/dt/1e6:.1f} Mrays/s  {st.samples/dt/1e6:.1f} Msamples/s", flush=True)
+img = out.cpu().numpy()
+print("mean rgb", img[..., :3].mean(axis=(0, 1)), "finite", bool(np.isfinite(img).all()))

@@ -1,0 +1,21 @@
+"""Test configuration: `gpu` marks tests that need an MI355X (run with -m gpu on the GPU box)."""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "hyper-ray-tracer_amd"))
+sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an AMD GPU (MI355X); runs via gpurun")
+    config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+@pytest.fixture(scope="session")
+def earth():
+    import hrt
+
+    return hrt.synthetic_earth()
