@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -722,9 +723,17 @@ hrt_status device_upload(hrt_scene* s, int device) {
     put(s->off_texs, s->g_texs.data(), s->g_texs.size() * sizeof(G::Tex));
     put(s->off_perlin, s->perlin.data(), s->perlin.size() * sizeof(G::Perlin));
     put(s->off_images, s->images.data(), s->images.size());
+    s->device = device; /* from here on device_release() cleans up whatever was allocated */
     hip_check(hipMalloc(&s->d_blob, off), "hipMalloc(scene)");
     hip_check(hipMemcpy(s->d_blob, blob.data(), off, hipMemcpyHostToDevice), "hipMemcpy(scene)");
-    s->device = device;
+    s->slot_mutex = new std::mutex();
+    for (auto& sl : s->slots) {
+      hipEvent_t ev;
+      hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+      sl.event = ev;
+      sl.used = false;
+      sl.tiles_cap = 0;
+    }
   });
 }
 
@@ -733,6 +742,17 @@ void device_release(hrt_scene* s) {
   int prev = -1;
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(s->device);
+  for (auto& sl : s->slots) {
+    if (sl.event) {
+      (void)hipEventSynchronize((hipEvent_t)sl.event);
+      (void)hipEventDestroy((hipEvent_t)sl.event);
+    }
+    if (sl.d_mem) (void)hipFree(sl.d_mem);
+    if (sl.h_tiles) (void)hipHostFree(sl.h_tiles);
+    sl = hrt_scene::Slot();
+  }
+  delete static_cast<std::mutex*>(s->slot_mutex);
+  s->slot_mutex = nullptr;
   if (s->d_blob) (void)hipFree(s->d_blob);
   s->d_blob = nullptr;
   if (prev >= 0) (void)hipSetDevice(prev);
@@ -767,13 +787,26 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     if (pad >= 0xFFFF0000ull) throw HipError{HRT_ERR_UNSUPPORTED, "more than 4G pixels in one call"};
     hipStream_t stream = (hipStream_t)stream_;
     DeviceGuard dg(s->device);
-    /* per-call scratch: [counter u32 | pad | stats 3 x u64] + tiles, stream-ordered */
+    /* scratch slot: device [counter u32 | pad | stats 3 x u64 | tiles], pinned host [stats | tiles] */
+    std::lock_guard<std::mutex> lock(*static_cast<std::mutex*>(s->slot_mutex));
+    hrt_scene::Slot& sl = s->slots[s->next_slot++ % hrt_scene::N_SLOTS];
+    if (sl.used) hip_check(hipEventSynchronize((hipEvent_t)sl.event), "hipEventSynchronize(slot)");
     size_t tiles_bytes = n_tiles * sizeof(G::TileDev);
-    void* scratch = nullptr;
-    hip_check(hipMallocAsync(&scratch, 64 + tiles_bytes, stream), "hipMallocAsync");
+    if (tiles_bytes > sl.tiles_cap) {
+      if (sl.d_mem) hip_check(hipFree(sl.d_mem), "hipFree(slot)");
+      if (sl.h_tiles) hip_check(hipHostFree(sl.h_tiles), "hipHostFree(slot)");
+      sl.d_mem = sl.h_tiles = nullptr;
+      sl.tiles_cap = 0;
+      size_t cap = std::max<size_t>(tiles_bytes, 64 * sizeof(G::TileDev));
+      hip_check(hipMalloc(&sl.d_mem, 64 + cap), "hipMalloc(slot)");
+      hip_check(hipHostMalloc(&sl.h_tiles, 64 + cap, hipHostMallocDefault), "hipHostMalloc(slot)");
+      sl.tiles_cap = cap;
+    }
+    void* scratch = sl.d_mem;
+    memcpy((uint8_t*)sl.h_tiles + 64, td.data(), tiles_bytes);
     hip_check(hipMemsetAsync(scratch, 0, 64, stream), "hipMemsetAsync");
-    hip_check(hipMemcpyAsync((uint8_t*)scratch + 64, td.data(), tiles_bytes, hipMemcpyHostToDevice, stream),
-              "hipMemcpyAsync(tiles)");
+    hip_check(hipMemcpyAsync((uint8_t*)scratch + 64, (uint8_t*)sl.h_tiles + 64, tiles_bytes, hipMemcpyHostToDevice,
+                             stream), "hipMemcpyAsync(tiles)");
     KParams kp;
     uint8_t* base = (uint8_t*)s->d_blob;
     kp.nodes = (const G::Node*)(base + s->off_nodes);
@@ -817,16 +850,16 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
       if (full) launch<G::CULL_REFERENCE, true>(kp, s->device, stream);
       else launch<G::CULL_REFERENCE, false>(kp, s->device, stream);
     }
+    unsigned long long* h = (unsigned long long*)sl.h_tiles;
+    if (stats) hip_check(hipMemcpyAsync(h, (uint8_t*)scratch + 8, 24, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(stats)");
+    hip_check(hipEventRecord((hipEvent_t)sl.event, stream), "hipEventRecord(slot)");
+    sl.used = true;
     if (stats) {
-      unsigned long long h[3];
-      hip_check(hipMemcpyAsync(h, (uint8_t*)scratch + 8, sizeof(h), hipMemcpyDeviceToHost, stream),
-                "hipMemcpyAsync(stats)");
-      hip_check(hipStreamSynchronize(stream), "hipStreamSynchronize");
+      hip_check(hipEventSynchronize((hipEvent_t)sl.event), "hipEventSynchronize(stats)");
       stats->segments = h[0];
       stats->samples = h[1];
       stats->pixels = h[2];
     }
-    hip_check(hipFreeAsync(scratch, stream), "hipFreeAsync");
   });
 }
 

@@ -94,11 +94,20 @@ struct hrt_scene {
   size_t blob_bytes = 0;
   size_t off_nodes = 0, off_prims = 0, off_insts = 0, off_media = 0, off_mats = 0, off_texs = 0,
          off_perlin = 0, off_images = 0;
-  void* d_scratch = nullptr; /* pixel counter + stats, per render call slot */
-  void* d_tiles = nullptr;
-  size_t tiles_cap = 0;
-  void* d_out = nullptr; /* staging for the host-output hrt_render */
-  size_t out_cap = 0;
+  /* Render scratch slots (allocated at commit, reused round-robin): device [counter | stats |
+   * tiles], a pinned host staging copy of the tile list, and the event that marks the end of the
+   * slot's last use.  A call waits for its slot's previous use, so calls on any streams are safe. */
+  struct Slot {
+    void* d_mem = nullptr;
+    void* h_tiles = nullptr;
+    size_t tiles_cap = 0;
+    void* event = nullptr; /* hipEvent_t */
+    bool used = false;
+  };
+  static constexpr int N_SLOTS = 4;
+  Slot slots[N_SLOTS];
+  unsigned next_slot = 0;
+  void* slot_mutex = nullptr; /* std::mutex*, owned by render.hip */
 };
 
 namespace hrt {

@@ -128,6 +128,14 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    # torch ships its own libamdhip64 (same soname libamdhip64.so.7 as /opt/rocm's).  Loading torch
+    # first makes libhrt bind to that already-loaded runtime: ONE HIP runtime per process, so torch
+    # device pointers and hipStream_t handles are valid in libhrt.  (Loaded the other way round,
+    # torch would map a second runtime by file name and fail to find the device.)
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(path):
         raise FileNotFoundError(f"{path} missing: build it with `make -C hyper-ray-tracer_amd` (or __graft_entry__.build())")
     L = ctypes.CDLL(path)

@@ -54,8 +54,9 @@ def test_preset_parity(name, w, h, spp, depth, earth):
 @pytest.mark.gpu
 def test_region_and_depth_cap(earth):
     """A sub-region renders the same pixels as the full frame; depth caps (incl. 1) match."""
-    full, _, _ = _gpu_render("random", 64, 36, 8, 3, 11, earth)
-    part, _, _ = _gpu_render("random", 64, 36, 8, 3, 11, earth, region=(10, 5, 20, 17))
+    full, st_full, _ = _gpu_render("random", 64, 36, 8, 3, 11, earth)
+    part, st_part, _ = _gpu_render("random", 64, 36, 8, 3, 11, earth, region=(10, 5, 20, 17))
+    assert st_full.pixels == 64 * 36 and st_part.pixels == 20 * 17, (st_full.pixels, st_part.pixels)
     assert np.array_equal(full[5:22, 10:30], part)
     o = O.OracleScene(0, 1, earth)
     for depth in (1, 2):
@@ -84,3 +85,60 @@ def test_device_math_bit_identical():
         d = hrt.device_math(op, x, y)
         h = O.math(op, x, y)
         assert np.array_equal(d.view(np.uint32), h.view(np.uint32)), f"op {op}: {np.sum(d != h)} differ"
+
+
+@pytest.mark.gpu
+def test_repeated_calls_on_two_streams(earth):
+    """Many back-to-back tile renders on two HIP streams (scratch-slot reuse) all match a single
+    full-frame render: the per-pixel RNG keys make tiles independent of call order and stream."""
+    import torch
+
+    s = hrt.preset("random", 1, earth)
+    s.commit()
+    W, H = 96, 54
+    cam = hrt.preset_camera(s.info, W, H)
+    p = hrt.params(W, H, 4, 8, 5, tuple(s.info.background))
+    full = hrt.render(s, cam, p)
+    tiles = hrt.tile_grid(W, H, 16)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = []
+    for rep in range(3):
+        for i, t in enumerate(tiles):
+            d = torch.full((t[3], t[2], 4), -7.0, device="cuda")
+            st = streams[(i + rep) % 2]
+            st.wait_stream(torch.cuda.current_stream())
+            hrt.render_tiles_device(s, cam, p, [t], d.data_ptr(), st.cuda_stream)
+            outs.append((t, d, st))
+    torch.cuda.synchronize()
+    for t, d, _ in outs:
+        x, y, w, h = t
+        assert np.array_equal(d.cpu().numpy(), full[y:y + h, x:x + w]), t
+
+
+@pytest.mark.gpu
+def test_multi_tile_call_matches_full_frame(earth):
+    """One call over a rank's interleaved tile subset (the multi-GPU split) packs tiles back to back
+    and reproduces the full-frame pixels bit for bit, for every rank of a 3-way split."""
+    import torch
+
+    s = hrt.preset("random", 1, earth)
+    s.commit()
+    W, H = 200, 90
+    cam = hrt.preset_camera(s.info, W, H)
+    p = hrt.params(W, H, 4, 8, 9, tuple(s.info.background))
+    full = hrt.render(s, cam, p)
+    covered = np.zeros((H, W), bool)
+    for rank in range(3):
+        tiles = hrt.tile_grid(W, H, 80, rank, 3)
+        n = sum(t[2] * t[3] for t in tiles)
+        d = torch.zeros(n * 4, device="cuda")
+        st = hrt.render_tiles_device(s, cam, p, tiles, d.data_ptr(), 0, want_stats=True)
+        assert st.pixels == n
+        flat = d.cpu().numpy()
+        off = 0
+        for x, y, w, h in tiles:
+            blk = flat[off * 4:(off + w * h) * 4].reshape(h, w, 4)
+            assert np.array_equal(blk, full[y:y + h, x:x + w])
+            covered[y:y + h, x:x + w] = True
+            off += w * h
+    assert covered.all()
