@@ -63,7 +63,15 @@ struct KParams {
   uint32_t total_work;
   float4* out;
   uint32_t* counter;
-  unsigned long long* stats; /* segments, samples, pixels */
+  unsigned long long* stats; /* segments, samples, pixels, then (COUNT builds) nodes, prims, tex */
+  /* sample chunks: a work item is (pixel, chunk of `chunk` consecutive samples) */
+  uint32_t chunk, n_chunks, n_out;
+  float4* partial; /* [n_chunks][n_out] chunk sums (n_chunks > 1) */
+};
+
+/* per-lane work counters of the instrumented (COUNT) instantiation */
+struct Counts {
+  uint32_t nodes, prims, tex;
 };
 
 struct TRay {
@@ -189,9 +197,9 @@ struct PathKey {
 /* The world walk.  Closest hit over [begin, end) of the node stream with t in [tmin, closest]:
  * `winner` = node index of the accepted leaf (NONE if nothing).  MEDIA: ConstantMedium nodes are
  * evaluated (their boundary walks are nested calls with MEDIA = false). */
-template <int CULL, bool FULL, bool MEDIA>
+template <int CULL, bool FULL, bool MEDIA, bool COUNT>
 __device__ void trace(const KParams& P, uint32_t begin, uint32_t end, Vec3 o, Vec3 d, float time,
-                      float tmin, float& closest, uint32_t& winner, const PathKey& pk) {
+                      float tmin, float& closest, uint32_t& winner, const PathKey& pk, Counts& cn) {
   TRay r;
   set_ray(r, o, d, time);
   Vec3 so[G::MAX_INST_DEPTH], sd[G::MAX_INST_DEPTH];
@@ -205,6 +213,7 @@ __device__ void trace(const KParams& P, uint32_t begin, uint32_t end, Vec3 o, Ve
     const uint32_t kind = kp >> 24;
     const uint32_t payload = kp & 0xFFFFFFu;
     const uint32_t here = i;
+    if constexpr (COUNT) cn.nodes++;
     if (kind <= G::K_BOX_PRIM) {
       bool pass = box_hit<CULL>(a, b, r, tmin, closest);
       if (kind == G::K_BOX) {
@@ -235,9 +244,9 @@ __device__ void trace(const KParams& P, uint32_t begin, uint32_t end, Vec3 o, Ve
             const float inf = __uint_as_float(0x7f800000u);
             float c1 = inf, c2 = inf;
             uint32_t w1 = G::NONE, w2 = G::NONE;
-            trace<CULL, FULL, false>(P, m.bstart, m.bend, r.o, r.d, r.time, -inf, c1, w1, pk);
+            trace<CULL, FULL, false, COUNT>(P, m.bstart, m.bend, r.o, r.d, r.time, -inf, c1, w1, pk, cn);
             if (w1 == G::NONE) continue;
-            trace<CULL, FULL, false>(P, m.bstart, m.bend, r.o, r.d, r.time, c1 + 0.0001f, c2, w2, pk);
+            trace<CULL, FULL, false, COUNT>(P, m.bstart, m.bend, r.o, r.d, r.time, c1 + 0.0001f, c2, w2, pk, cn);
             if (w2 == G::NONE) continue;
             float r1 = c1, r2 = c2;
             if (r1 < tmin) r1 = tmin;
@@ -260,6 +269,7 @@ __device__ void trace(const KParams& P, uint32_t begin, uint32_t end, Vec3 o, Ve
     const G::Prim* pp = P.prims + payload;
     const uint32_t km = pp->km;
     const uint32_t pkind = km & 3u;
+    if constexpr (COUNT) cn.prims++;
     float t;
     bool h;
     if (FULL && pkind == G::P_RECT) h = rect_t(pp, (km >> 2) & 3u, r, tmin, closest, t);
@@ -414,10 +424,11 @@ __device__ float perlin_noise(const G::Perlin* pn, Vec3 point) {
 }
 
 /* textures/.rs value() */
-template <bool FULL>
-__device__ Vec3 tex_value(const KParams& P, uint32_t id, float u, float v, Vec3 p) {
+template <bool FULL, bool COUNT>
+__device__ Vec3 tex_value(const KParams& P, uint32_t id, float u, float v, Vec3 p, Counts& cn) {
   for (int guard = 0; guard < 64; guard++) {
     const G::Tex& T = P.texs[id];
+    if constexpr (COUNT) cn.tex++;
     if (T.kind == G::T_SOLID) return v3(T.a[0], T.a[1], T.a[2]);
     if (T.kind == G::T_CHECKER) { /* checker_texture.rs:22-29 */
       float sines = sin_f(10.0f * p.x) * sin_f(10.0f * p.y) * sin_f(10.0f * p.z);
@@ -458,14 +469,14 @@ __device__ Vec3 tex_value(const KParams& P, uint32_t id, float u, float v, Vec3 
 }
 
 /* ------------------------------------------------------------------ the megakernel */
-template <int CULL, bool FULL>
+template <int CULL, bool FULL, bool COUNT>
 __global__ __launch_bounds__(256) void render_kernel(KParams P) {
   const uint32_t lane = threadIdx.x & 63u;
   const float scale = 1.0f / (float)P.spp; /* application.rs:403 */
   const float inf = __uint_as_float(0x7f800000u);
 
-  bool has_pixel = false, exhausted = false, in_path = false;
-  uint32_t px = 0, py = 0, out_idx = 0, sample = 0;
+  bool has_item = false, exhausted = false, in_path = false;
+  uint32_t px = 0, py = 0, out_idx = 0, chunk = 0, sample = 0, sample_end = 0;
   Vec3 sum = v3(0.0f, 0.0f, 0.0f);
   Rng rng;
   rng.s0 = rng.s1 = rng.s2 = rng.s3 = 1u;
@@ -475,10 +486,11 @@ __global__ __launch_bounds__(256) void render_kernel(KParams P) {
   float rtime = 0.0f;
   Vec3 thr = v3(1.0f, 1.0f, 1.0f), rad = v3(0.0f, 0.0f, 0.0f);
   uint32_t n_seg = 0, n_samples = 0, n_pixels = 0;
+  Counts cn{0u, 0u, 0u};
 
   for (;;) {
-    /* ---- claim pixels for idle lanes: one atomic per wave ---- */
-    const bool want = !has_pixel && !exhausted;
+    /* ---- claim work items for idle lanes: one atomic per wave ---- */
+    const bool want = !has_item && !exhausted;
     const unsigned long long want_mask = __ballot(want);
     if (want_mask) {
       const uint32_t cnt = (uint32_t)__popcll(want_mask);
@@ -492,29 +504,33 @@ __global__ __launch_bounds__(256) void render_kernel(KParams P) {
         if (w >= P.total_work) {
           exhausted = true;
         } else {
-          /* tile lookup (binary search on pad_start) then 8x8 block order inside the tile */
+          /* tile (binary search on pad_start), then [8x8 block][chunk][64 pixels] inside it */
           uint32_t lo = 0, hi = P.n_tiles - 1;
           while (lo < hi) {
             uint32_t mid = (lo + hi + 1) >> 1;
             if (P.tiles[mid].pad_start <= w) lo = mid; else hi = mid - 1;
           }
           const G::TileDev T = P.tiles[lo];
-          const uint32_t q = w - T.pad_start, blk = q >> 6, in = q & 63u;
+          const uint32_t q = w - T.pad_start;
+          const uint32_t blk = q / (64u * P.n_chunks), rem = q - blk * 64u * P.n_chunks;
+          const uint32_t c = rem >> 6, in = rem & 63u;
           const uint32_t lx = (blk % T.bw) * 8u + (in & 7u), ly = (blk / T.bw) * 8u + (in >> 3);
           if (lx < T.w && ly < T.h) {
-            has_pixel = true;
+            has_item = true;
             px = T.x + lx;
             py = T.y + ly;
             out_idx = T.out_off + ly * T.w + lx;
-            sample = 0;
+            chunk = c;
+            sample = c * P.chunk;
+            sample_end = min(P.spp, sample + P.chunk);
             sum = v3(0.0f, 0.0f, 0.0f);
             in_path = false;
           }
         }
       }
     }
-    if (!__any(has_pixel || !exhausted)) break;
-    if (!has_pixel) continue;
+    if (!__any(has_item || !exhausted)) break;
+    if (!has_item) continue;
 
     /* ---- start the next sample (application.rs:444-447, camera.rs:85-95) ---- */
     if (!in_path) {
@@ -542,7 +558,7 @@ __global__ __launch_bounds__(256) void render_kernel(KParams P) {
     } else {
       float closest = inf;
       uint32_t winner = G::NONE;
-      trace<CULL, FULL, FULL>(P, 0u, P.main_end, ro, rd, rtime, P.t_min, closest, winner, pk);
+      trace<CULL, FULL, FULL, COUNT>(P, 0u, P.main_end, ro, rd, rtime, P.t_min, closest, winner, pk, cn);
       n_seg++;
       pk.segment++;
       if (winner == G::NONE) {
@@ -557,7 +573,7 @@ __global__ __launch_bounds__(256) void render_kernel(KParams P) {
         if (M.kind == G::M_LAMBERTIAN) { /* lambertian.rs:27-38 */
           ndir = rec.n + random_unit_vector(rng);
           if (near_zero(ndir)) ndir = rec.n;
-          att = tex_value<FULL>(P, M.tex, rec.u, rec.v, rec.p);
+          att = tex_value<FULL, COUNT>(P, M.tex, rec.u, rec.v, rec.p, cn);
           scattered = true;
         } else if (M.kind == G::M_METAL) { /* metal.rs:29-42 */
           Vec3 reflected = reflect(normalize(rd), rec.n);
@@ -575,9 +591,9 @@ __global__ __launch_bounds__(256) void render_kernel(KParams P) {
           att = v3(1.0f, 1.0f, 1.0f);
           scattered = true;
         } else if (FULL && M.kind == G::M_DIFFUSE_LIGHT) { /* diffuse_light.rs:20-28 */
-          emitted = tex_value<FULL>(P, M.tex, rec.u, rec.v, rec.p);
+          emitted = tex_value<FULL, COUNT>(P, M.tex, rec.u, rec.v, rec.p, cn);
         } else if (FULL && M.kind == G::M_ISOTROPIC) { /* isotropic.rs:26-33 */
-          att = tex_value<FULL>(P, M.tex, rec.u, rec.v, rec.p);
+          att = tex_value<FULL, COUNT>(P, M.tex, rec.u, rec.v, rec.p, cn);
           ndir = random_in_unit_sphere(rng);
           scattered = true;
         }
@@ -594,19 +610,45 @@ __global__ __launch_bounds__(256) void render_kernel(KParams P) {
       }
     }
     if (done) {
-      sum = sum + rad;
+      sum = sum + rad; /* application.rs:448, samples of a chunk in order */
       in_path = false;
       n_samples++;
-      if (++sample == P.spp) {
-        P.out[out_idx] = make_float4(sqrtf(sum.x * scale), sqrtf(sum.y * scale), sqrtf(sum.z * scale), 1.0f);
-        has_pixel = false;
-        n_pixels++;
+      if (++sample == sample_end) {
+        if (P.n_chunks == 1) {
+          P.out[out_idx] = make_float4(sqrtf(sum.x * scale), sqrtf(sum.y * scale), sqrtf(sum.z * scale), 1.0f);
+          n_pixels++;
+        } else {
+          P.partial[(size_t)chunk * P.n_out + out_idx] = make_float4(sum.x, sum.y, sum.z, 0.0f);
+          if (chunk == 0) n_pixels++;
+        }
+        has_item = false;
       }
     }
   }
   atomicAdd(&P.stats[0], (unsigned long long)n_seg);
   atomicAdd(&P.stats[1], (unsigned long long)n_samples);
   atomicAdd(&P.stats[2], (unsigned long long)n_pixels);
+  if constexpr (COUNT) {
+    atomicAdd(&P.stats[3], (unsigned long long)cn.nodes);
+    atomicAdd(&P.stats[4], (unsigned long long)cn.prims);
+    atomicAdd(&P.stats[5], (unsigned long long)cn.tex);
+  }
+}
+
+/* chunk sums -> pixel, in chunk order (fixed, so 1/2/4/8-GPU splits give identical bits);
+ * then sqrt(sum * (1/spp)) with alpha 1 (application.rs:451-456) */
+__global__ __launch_bounds__(256) void reduce_chunks(const float4* __restrict__ partial, float4* __restrict__ out,
+                                                     uint32_t n_out, uint32_t n_chunks, uint32_t spp) {
+  const float scale = 1.0f / (float)spp;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_out; i += gridDim.x * blockDim.x) {
+    float4 a = partial[i];
+    Vec3 sum = v3(a.x, a.y, a.z);
+    for (uint32_t c = 1; c < n_chunks; c++) {
+      float4 b = partial[(size_t)c * n_out + i];
+      sum = sum + v3(b.x, b.y, b.z);
+    }
+    out[i] = make_float4(sqrtf(sum.x * scale), sqrtf(sum.y * scale), sqrtf(sum.z * scale), 1.0f);
+  }
 }
 
 __global__ void math_kernel(int op, const float* x, const float* y, float* out, uint32_t n) {
@@ -665,12 +707,12 @@ hrt_status hguard(F&& f) {
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-template <int CULL, bool FULL>
+template <int CULL, bool FULL, bool COUNT>
 int resident_grid(int device) {
   static int cached[64] = {0};
   if (device >= 0 && device < 64 && cached[device]) return cached[device];
   int per_cu = 0;
-  hip_check(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_kernel<CULL, FULL>, 256, 0),
+  hip_check(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_kernel<CULL, FULL, COUNT>, 256, 0),
             "hipOccupancyMaxActiveBlocksPerMultiprocessor");
   hipDeviceProp_t prop;
   hip_check(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
@@ -679,11 +721,23 @@ int resident_grid(int device) {
   return g;
 }
 
-template <int CULL, bool FULL>
+template <int CULL, bool FULL, bool COUNT>
 void launch(const KParams& kp, int device, hipStream_t stream) {
-  int grid = resident_grid<CULL, FULL>(device);
-  hipLaunchKernelGGL((render_kernel<CULL, FULL>), dim3(grid), dim3(256), 0, stream, kp);
+  int grid = resident_grid<CULL, FULL, COUNT>(device);
+  hipLaunchKernelGGL((render_kernel<CULL, FULL, COUNT>), dim3(grid), dim3(256), 0, stream, kp);
   hip_check(hipGetLastError(), "render_kernel launch");
+}
+
+template <bool COUNT>
+void launch_any(const hrt_scene* s, const KParams& kp, hipStream_t stream) {
+  const bool full = (s->feature_mask & ~G::F_BASIC) != 0;
+  if (s->cull_mode == G::CULL_SLAB) {
+    if (full) launch<G::CULL_SLAB, true, COUNT>(kp, s->device, stream);
+    else launch<G::CULL_SLAB, false, COUNT>(kp, s->device, stream);
+  } else {
+    if (full) launch<G::CULL_REFERENCE, true, COUNT>(kp, s->device, stream);
+    else launch<G::CULL_REFERENCE, false, COUNT>(kp, s->device, stream);
+  }
 }
 
 }  // namespace
@@ -748,6 +802,7 @@ void device_release(hrt_scene* s) {
       (void)hipEventDestroy((hipEvent_t)sl.event);
     }
     if (sl.d_mem) (void)hipFree(sl.d_mem);
+    if (sl.d_partial) (void)hipFree(sl.d_partial);
     if (sl.h_tiles) (void)hipHostFree(sl.h_tiles);
     sl = hrt_scene::Slot();
   }
@@ -770,9 +825,14 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     if (!s || !cam || !p || !tiles || !d_rgba || n_tiles == 0)
       throw HipError{HRT_ERR_INVALID_ARG, "hrt_render_tiles_device: null argument"};
     if (!s->committed || !s->d_blob) throw HipError{HRT_ERR_STATE, "scene not committed"};
-    if (p->width < 2 || p->height < 2 || p->samples == 0 || p->flags != 0)
-      throw HipError{HRT_ERR_INVALID_ARG, "bad render params (width/height >= 2, samples > 0, flags == 0)"};
+    if (p->width < 2 || p->height < 2 || p->samples == 0 || (p->flags & ~(uint32_t)HRT_RENDER_COUNT_WORK) != 0)
+      throw HipError{HRT_ERR_INVALID_ARG, "bad render params (width/height >= 2, samples > 0, known flags)"};
     if (!(cam->time0 < cam->time1)) throw HipError{HRT_ERR_INVALID_ARG, "camera time0 must be < time1"};
+    /* sample chunks: spp <= 32 keeps one work item per pixel (the reference's sequential sum);
+     * larger spp splits into <= 16 chunks so the frame's tail is a chunk, not a whole pixel */
+    const uint32_t spp = p->samples;
+    const uint32_t chunk = spp <= 32 ? spp : std::max<uint32_t>(32, (spp + 15) / 16);
+    const uint32_t n_chunks = (spp + chunk - 1) / chunk;
     std::vector<G::TileDev> td(n_tiles);
     uint64_t pad = 0, outp = 0;
     for (uint32_t i = 0; i < n_tiles; i++) {
@@ -781,7 +841,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
         throw HipError{HRT_ERR_INVALID_ARG, "tile outside the image"};
       uint32_t bw = (t.w + 7) / 8, bh = (t.h + 7) / 8;
       td[i] = G::TileDev{t.x, t.y, t.w, t.h, bw, (uint32_t)pad, (uint32_t)outp, 0};
-      pad += (uint64_t)bw * bh * 64;
+      pad += (uint64_t)bw * bh * 64 * n_chunks;
       outp += (uint64_t)t.w * t.h;
     }
     if (pad >= 0xFFFF0000ull) throw HipError{HRT_ERR_UNSUPPORTED, "more than 4G pixels in one call"};
@@ -801,6 +861,14 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
       hip_check(hipMalloc(&sl.d_mem, 64 + cap), "hipMalloc(slot)");
       hip_check(hipHostMalloc(&sl.h_tiles, 64 + cap, hipHostMallocDefault), "hipHostMalloc(slot)");
       sl.tiles_cap = cap;
+    }
+    const size_t partial_bytes = n_chunks > 1 ? (size_t)n_chunks * outp * sizeof(float4) : 0;
+    if (partial_bytes > sl.partial_cap) {
+      if (sl.d_partial) hip_check(hipFree(sl.d_partial), "hipFree(partial)");
+      sl.d_partial = nullptr;
+      sl.partial_cap = 0;
+      hip_check(hipMalloc(&sl.d_partial, partial_bytes), "hipMalloc(partial)");
+      sl.partial_cap = partial_bytes;
     }
     void* scratch = sl.d_mem;
     memcpy((uint8_t*)sl.h_tiles + 64, td.data(), tiles_bytes);
@@ -842,16 +910,20 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     kp.out = (float4*)d_rgba;
     kp.counter = (uint32_t*)scratch;
     kp.stats = (unsigned long long*)((uint8_t*)scratch + 8);
-    const bool full = (s->feature_mask & ~G::F_BASIC) != 0;
-    if (s->cull_mode == G::CULL_SLAB) {
-      if (full) launch<G::CULL_SLAB, true>(kp, s->device, stream);
-      else launch<G::CULL_SLAB, false>(kp, s->device, stream);
-    } else {
-      if (full) launch<G::CULL_REFERENCE, true>(kp, s->device, stream);
-      else launch<G::CULL_REFERENCE, false>(kp, s->device, stream);
+    kp.chunk = chunk;
+    kp.n_chunks = n_chunks;
+    kp.n_out = (uint32_t)outp;
+    kp.partial = (float4*)sl.d_partial;
+    if (p->flags & HRT_RENDER_COUNT_WORK) launch_any<true>(s, kp, stream);
+    else launch_any<false>(s, kp, stream);
+    if (n_chunks > 1) {
+      uint32_t blocks = (uint32_t)std::min<uint64_t>((outp + 255) / 256, 4096);
+      hipLaunchKernelGGL(reduce_chunks, dim3(blocks), dim3(256), 0, stream, (const float4*)sl.d_partial,
+                         (float4*)d_rgba, (uint32_t)outp, n_chunks, spp);
+      hip_check(hipGetLastError(), "reduce_chunks launch");
     }
     unsigned long long* h = (unsigned long long*)sl.h_tiles;
-    if (stats) hip_check(hipMemcpyAsync(h, (uint8_t*)scratch + 8, 24, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(stats)");
+    if (stats) hip_check(hipMemcpyAsync(h, (uint8_t*)scratch + 8, 48, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(stats)");
     hip_check(hipEventRecord((hipEvent_t)sl.event, stream), "hipEventRecord(slot)");
     sl.used = true;
     if (stats) {
@@ -859,6 +931,9 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
       stats->segments = h[0];
       stats->samples = h[1];
       stats->pixels = h[2];
+      stats->node_visits = h[3];
+      stats->prim_tests = h[4];
+      stats->tex_evals = h[5];
     }
   });
 }

@@ -102,6 +102,8 @@ struct hrt_scene {
     void* h_tiles = nullptr;
     size_t tiles_cap = 0;
     void* event = nullptr; /* hipEvent_t */
+    void* d_partial = nullptr; /* sample-chunk sums [n_chunks][pixels] */
+    size_t partial_cap = 0;
     bool used = false;
   };
   static constexpr int N_SLOTS = 4;

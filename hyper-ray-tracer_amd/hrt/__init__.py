@@ -82,7 +82,7 @@ class Tile(ctypes.Structure):
 
 
 class RenderStats(ctypes.Structure):
-    _fields_ = [("segments", ctypes.c_uint64), ("samples", ctypes.c_uint64), ("pixels", ctypes.c_uint64)]
+    _fields_ = [(n, ctypes.c_uint64) for n in ("segments", "samples", "pixels", "node_visits", "prim_tests", "tex_evals")]
 
 
 class PresetInfo(ctypes.Structure):
@@ -350,10 +350,13 @@ def preset_camera(info: PresetInfo, width: int, height: int) -> Camera:
     return camera(info.look_from, info.look_at, info.fov, info.aperture, info.focus_dist, info.time0, info.time1, width, height)
 
 
-def params(width, height, samples, max_depth=50, seed=1, background=(0.7, 0.8, 1.0), t_min=0.001, sample_offset=0) -> RenderParams:
+RENDER_COUNT_WORK = 1
+
+
+def params(width, height, samples, max_depth=50, seed=1, background=(0.7, 0.8, 1.0), t_min=0.001, sample_offset=0, flags=0) -> RenderParams:
     p = RenderParams()
     p.width, p.height, p.samples, p.max_depth = width, height, samples, max_depth
-    p.sample_offset, p.flags, p.t_min, p.seed = sample_offset, 0, t_min, seed
+    p.sample_offset, p.flags, p.t_min, p.seed = sample_offset, flags, t_min, seed
     for i in range(3):
         p.background[i] = float(background[i])
     return p

@@ -71,11 +71,17 @@ typedef struct hrt_render_params {
   uint32_t samples;         /* spp (application.rs:443) */
   uint32_t max_depth;       /* ray_color depth (application.rs:478); reference CLI default 10 */
   uint32_t sample_offset;   /* first sample index (0; >0 splits one pixel's samples across jobs) */
-  uint32_t flags;           /* reserved, must be 0 */
+  uint32_t flags;           /* HRT_RENDER_* bits */
   float t_min;              /* 0.001 */
   float background[3];
   uint64_t seed;
 } hrt_render_params;
+
+/* hrt_render_params.flags */
+enum {
+  HRT_RENDER_COUNT_WORK = 1 /* instrumented kernel: stats also count node visits / prim tests / texture
+                               evaluations (for the algorithmic-bytes model; slower) */
+};
 
 typedef struct hrt_tile {
   uint32_t x, y, w, h; /* image coordinates, y up */
@@ -86,6 +92,9 @@ typedef struct hrt_render_stats {
   uint64_t segments;        /* world.hit calls == rays (application.rs:482) */
   uint64_t samples;         /* primary samples = pixels * spp */
   uint64_t pixels;
+  uint64_t node_visits;     /* HRT_RENDER_COUNT_WORK only: node-stream entries read */
+  uint64_t prim_tests;      /* HRT_RENDER_COUNT_WORK only: primitive intersection tests */
+  uint64_t tex_evals;       /* HRT_RENDER_COUNT_WORK only: Texture::value evaluations */
 } hrt_render_stats;
 
 /* Scene description of one reference preset (application.rs:132-211). */

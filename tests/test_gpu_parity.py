@@ -13,8 +13,11 @@ from oracle import oracle as O
 
 TOL = 1e-3
 
-# (preset, width, height, spp, depth): every scene feature of the reference
+# (preset, width, height, spp, depth): every scene feature of the reference; spp > 32 exercises the
+# sample-chunk split (chunk sums reduced in a fixed order)
 CASES = [
+    ("random", 40, 24, 100, 50),
+    ("cornell", 24, 24, 70, 50),
     ("random", 64, 36, 16, 50),
     ("two_spheres", 48, 27, 16, 50),
     ("two_perlin_spheres", 48, 27, 16, 50),
