@@ -66,6 +66,7 @@ struct KParams {
   unsigned long long* stats; /* segments, samples, pixels, then (COUNT builds) nodes, prims, tex */
   /* sample chunks: a work item is (pixel, chunk of `chunk` consecutive samples) */
   uint32_t chunk, n_chunks, n_out;
+  uint32_t n_prims;
   float4* partial; /* [n_chunks][n_out] chunk sums (n_chunks > 1) */
 };
 
@@ -198,15 +199,16 @@ struct PathKey {
  * `winner` = node index of the accepted leaf (NONE if nothing).  MEDIA: ConstantMedium nodes are
  * evaluated (their boundary walks are nested calls with MEDIA = false). */
 template <int CULL, bool FULL, bool MEDIA, bool COUNT>
-__device__ void trace(const KParams& P, uint32_t begin, uint32_t end, Vec3 o, Vec3 d, float time,
-                      float tmin, float& closest, uint32_t& winner, const PathKey& pk, Counts& cn) {
+__device__ void trace(const KParams& P, const G::Node* __restrict__ nodes, const G::Prim* __restrict__ prims,
+                      uint32_t begin, uint32_t end, Vec3 o, Vec3 d, float time, float tmin, float& closest,
+                      uint32_t& winner, const PathKey& pk, Counts& cn) {
   TRay r;
   set_ray(r, o, d, time);
   Vec3 so[G::MAX_INST_DEPTH], sd[G::MAX_INST_DEPTH];
   int sp = 0;
   uint32_t i = begin;
   while (i < end) {
-    const G::Node* np = P.nodes + i;
+    const G::Node* np = nodes + i;
     const float4 a = ld4(np->mn);
     const float4 b = ld4(np->mx);
     const uint32_t kp = __float_as_uint(b.w);
@@ -244,9 +246,9 @@ __device__ void trace(const KParams& P, uint32_t begin, uint32_t end, Vec3 o, Ve
             const float inf = __uint_as_float(0x7f800000u);
             float c1 = inf, c2 = inf;
             uint32_t w1 = G::NONE, w2 = G::NONE;
-            trace<CULL, FULL, false, COUNT>(P, m.bstart, m.bend, r.o, r.d, r.time, -inf, c1, w1, pk, cn);
+            trace<CULL, FULL, false, COUNT>(P, nodes, prims, m.bstart, m.bend, r.o, r.d, r.time, -inf, c1, w1, pk, cn);
             if (w1 == G::NONE) continue;
-            trace<CULL, FULL, false, COUNT>(P, m.bstart, m.bend, r.o, r.d, r.time, c1 + 0.0001f, c2, w2, pk, cn);
+            trace<CULL, FULL, false, COUNT>(P, nodes, prims, m.bstart, m.bend, r.o, r.d, r.time, c1 + 0.0001f, c2, w2, pk, cn);
             if (w2 == G::NONE) continue;
             float r1 = c1, r2 = c2;
             if (r1 < tmin) r1 = tmin;
@@ -266,7 +268,7 @@ __device__ void trace(const KParams& P, uint32_t begin, uint32_t end, Vec3 o, Ve
       continue;
     }
     /* one primitive (payload) */
-    const G::Prim* pp = P.prims + payload;
+    const G::Prim* pp = prims + payload;
     const uint32_t km = pp->km;
     const uint32_t pkind = km & 3u;
     if constexpr (COUNT) cn.prims++;
@@ -469,8 +471,24 @@ __device__ Vec3 tex_value(const KParams& P, uint32_t id, float u, float v, Vec3 
 }
 
 /* ------------------------------------------------------------------ the megakernel */
-template <int CULL, bool FULL, bool COUNT>
-__global__ __launch_bounds__(256) void render_kernel(KParams P) {
+/* LDS: the node stream and primitive records are copied into LDS once per workgroup (they are
+ * read ~60 times per ray by dependent loads; LDS latency is a fraction of an L2 hit). */
+template <int CULL, bool FULL, bool COUNT, bool LDS>
+__global__ __launch_bounds__(LDS ? 512 : 256) void render_kernel(KParams P) {
+  extern __shared__ float4 lds_scene[];
+  const G::Node* nodes = P.nodes;
+  const G::Prim* prims = P.prims;
+  if constexpr (LDS) {
+    const uint32_t n4 = P.main_end * (uint32_t)(sizeof(G::Node) / 16);
+    const uint32_t p4 = P.n_prims * (uint32_t)(sizeof(G::Prim) / 16);
+    const float4* gn = reinterpret_cast<const float4*>(P.nodes);
+    const float4* gp = reinterpret_cast<const float4*>(P.prims);
+    for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) lds_scene[k] = gn[k];
+    for (uint32_t k = threadIdx.x; k < p4; k += blockDim.x) lds_scene[n4 + k] = gp[k];
+    __syncthreads();
+    nodes = reinterpret_cast<const G::Node*>(lds_scene);
+    prims = reinterpret_cast<const G::Prim*>(lds_scene + n4);
+  }
   const uint32_t lane = threadIdx.x & 63u;
   const float scale = 1.0f / (float)P.spp; /* application.rs:403 */
   const float inf = __uint_as_float(0x7f800000u);
@@ -558,7 +576,7 @@ __global__ __launch_bounds__(256) void render_kernel(KParams P) {
     } else {
       float closest = inf;
       uint32_t winner = G::NONE;
-      trace<CULL, FULL, FULL, COUNT>(P, 0u, P.main_end, ro, rd, rtime, P.t_min, closest, winner, pk, cn);
+      trace<CULL, FULL, FULL, COUNT>(P, nodes, prims, 0u, P.main_end, ro, rd, rtime, P.t_min, closest, winner, pk, cn);
       n_seg++;
       pk.segment++;
       if (winner == G::NONE) {
@@ -707,36 +725,54 @@ hrt_status hguard(F&& f) {
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-template <int CULL, bool FULL, bool COUNT>
-int resident_grid(int device) {
+template <int CULL, bool FULL, bool COUNT, bool LDS>
+int resident_grid(int device, size_t smem) {
   static int cached[64] = {0};
-  if (device >= 0 && device < 64 && cached[device]) return cached[device];
+  static size_t cached_smem[64] = {0};
+  if (device >= 0 && device < 64 && cached[device] && cached_smem[device] == smem) return cached[device];
+  auto fn = render_kernel<CULL, FULL, COUNT, LDS>;
+  const int block = LDS ? 512 : 256;
+  if (LDS) hip_check(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem),
+                     "hipFuncSetAttribute(LDS)");
   int per_cu = 0;
-  hip_check(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_kernel<CULL, FULL, COUNT>, 256, 0),
+  hip_check(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block, smem),
             "hipOccupancyMaxActiveBlocksPerMultiprocessor");
   hipDeviceProp_t prop;
   hip_check(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
   int g = std::max(1, per_cu) * prop.multiProcessorCount;
-  if (device >= 0 && device < 64) cached[device] = g;
+  if (device >= 0 && device < 64) { cached[device] = g; cached_smem[device] = smem; }
   return g;
 }
 
-template <int CULL, bool FULL, bool COUNT>
-void launch(const KParams& kp, int device, hipStream_t stream) {
-  int grid = resident_grid<CULL, FULL, COUNT>(device);
-  hipLaunchKernelGGL((render_kernel<CULL, FULL, COUNT>), dim3(grid), dim3(256), 0, stream, kp);
+template <int CULL, bool FULL, bool COUNT, bool LDS>
+void launch(const KParams& kp, int device, hipStream_t stream, size_t smem) {
+  int grid = resident_grid<CULL, FULL, COUNT, LDS>(device, smem);
+  hipLaunchKernelGGL((render_kernel<CULL, FULL, COUNT, LDS>), dim3(grid), dim3(LDS ? 512 : 256), LDS ? smem : 0,
+                     stream, kp);
   hip_check(hipGetLastError(), "render_kernel launch");
 }
 
+/* LDS residency: the traversed node stream + primitives must fit twice per CU (two 512-thread
+ * workgroups, 160 KiB LDS per CU). */
+constexpr size_t LDS_SCENE_MAX = 72 * 1024;
+
+size_t lds_bytes(const hrt_scene* s) {
+  return s->main_end * sizeof(G::Node) + s->g_prims.size() * sizeof(G::Prim);
+}
+
 template <bool COUNT>
-void launch_any(const hrt_scene* s, const KParams& kp, hipStream_t stream) {
+void launch_any(const hrt_scene* s, const KParams& kp, hipStream_t stream, bool allow_lds) {
   const bool full = (s->feature_mask & ~G::F_BASIC) != 0;
+  const size_t smem = lds_bytes(s);
+  const bool lds = allow_lds && !full && smem <= LDS_SCENE_MAX;
   if (s->cull_mode == G::CULL_SLAB) {
-    if (full) launch<G::CULL_SLAB, true, COUNT>(kp, s->device, stream);
-    else launch<G::CULL_SLAB, false, COUNT>(kp, s->device, stream);
+    if (full) launch<G::CULL_SLAB, true, COUNT, false>(kp, s->device, stream, 0);
+    else if (lds) launch<G::CULL_SLAB, false, COUNT, true>(kp, s->device, stream, smem);
+    else launch<G::CULL_SLAB, false, COUNT, false>(kp, s->device, stream, 0);
   } else {
-    if (full) launch<G::CULL_REFERENCE, true, COUNT>(kp, s->device, stream);
-    else launch<G::CULL_REFERENCE, false, COUNT>(kp, s->device, stream);
+    if (full) launch<G::CULL_REFERENCE, true, COUNT, false>(kp, s->device, stream, 0);
+    else if (lds) launch<G::CULL_REFERENCE, false, COUNT, true>(kp, s->device, stream, smem);
+    else launch<G::CULL_REFERENCE, false, COUNT, false>(kp, s->device, stream, 0);
   }
 }
 
@@ -825,7 +861,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     if (!s || !cam || !p || !tiles || !d_rgba || n_tiles == 0)
       throw HipError{HRT_ERR_INVALID_ARG, "hrt_render_tiles_device: null argument"};
     if (!s->committed || !s->d_blob) throw HipError{HRT_ERR_STATE, "scene not committed"};
-    if (p->width < 2 || p->height < 2 || p->samples == 0 || (p->flags & ~(uint32_t)HRT_RENDER_COUNT_WORK) != 0)
+    if (p->width < 2 || p->height < 2 || p->samples == 0 || (p->flags & ~(uint32_t)(HRT_RENDER_COUNT_WORK | HRT_RENDER_NO_LDS)) != 0)
       throw HipError{HRT_ERR_INVALID_ARG, "bad render params (width/height >= 2, samples > 0, known flags)"};
     if (!(cam->time0 < cam->time1)) throw HipError{HRT_ERR_INVALID_ARG, "camera time0 must be < time1"};
     /* sample chunks: spp <= 32 keeps one work item per pixel (the reference's sequential sum);
@@ -914,8 +950,10 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     kp.n_chunks = n_chunks;
     kp.n_out = (uint32_t)outp;
     kp.partial = (float4*)sl.d_partial;
-    if (p->flags & HRT_RENDER_COUNT_WORK) launch_any<true>(s, kp, stream);
-    else launch_any<false>(s, kp, stream);
+    kp.n_prims = (uint32_t)s->g_prims.size();
+    const bool allow_lds = (p->flags & HRT_RENDER_NO_LDS) == 0;
+    if (p->flags & HRT_RENDER_COUNT_WORK) launch_any<true>(s, kp, stream, allow_lds);
+    else launch_any<false>(s, kp, stream, allow_lds);
     if (n_chunks > 1) {
       uint32_t blocks = (uint32_t)std::min<uint64_t>((outp + 255) / 256, 4096);
       hipLaunchKernelGGL(reduce_chunks, dim3(blocks), dim3(256), 0, stream, (const float4*)sl.d_partial,

@@ -770,7 +770,8 @@ hrt_status hrt_scene_get_info(const hrt_scene* s, hrt_scene_info* info) {
     info->media = (uint32_t)s->g_media.size();
     info->feature_mask = s->feature_mask;
     info->blob_bytes = (uint32_t)s->blob_bytes;
-    info->in_lds = 0;
+    info->in_lds = ((s->feature_mask & ~G::F_BASIC) == 0 &&
+                    s->main_end * sizeof(G::Node) + s->g_prims.size() * sizeof(G::Prim) <= 72 * 1024) ? 1u : 0u;
     info->cull_mode = (uint32_t)s->cull_mode;
   });
 }

@@ -351,6 +351,7 @@ def preset_camera(info: PresetInfo, width: int, height: int) -> Camera:
 
 
 RENDER_COUNT_WORK = 1
+RENDER_NO_LDS = 2
 
 
 def params(width, height, samples, max_depth=50, seed=1, background=(0.7, 0.8, 1.0), t_min=0.001, sample_offset=0, flags=0) -> RenderParams:

@@ -79,8 +79,9 @@ typedef struct hrt_render_params {
 
 /* hrt_render_params.flags */
 enum {
-  HRT_RENDER_COUNT_WORK = 1 /* instrumented kernel: stats also count node visits / prim tests / texture
-                               evaluations (for the algorithmic-bytes model; slower) */
+  HRT_RENDER_COUNT_WORK = 1, /* instrumented kernel: stats also count node visits / prim tests / texture
+                                evaluations (for the algorithmic-bytes model; slower) */
+  HRT_RENDER_NO_LDS = 2      /* keep the scene in global memory even when it fits in LDS (A/B) */
 };
 
 typedef struct hrt_tile {

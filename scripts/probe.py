@@ -17,6 +17,7 @@ ap.add_argument("--height", type=int, default=1080)
 ap.add_argument("--spp", type=int, default=16)
 ap.add_argument("--depth", type=int, default=50)
 ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--ab", default="", help="comma list of flag values to alternate (A/B in one process)")
 a = ap.parse_args()
 
 s = hrt.preset(a.preset, 1)
@@ -24,16 +25,24 @@ s.commit(0)
 si = s.scene_info()
 print(f"scene {a.preset}: nodes {si.nodes} prims {si.prims} features {si.feature_mask:#x} cull {si.cull_mode} blob {si.blob_bytes} B", flush=True)
 cam = hrt.preset_camera(s.info, a.width, a.height)
-p = hrt.params(a.width, a.height, a.spp, a.depth, 1, tuple(s.info.background))
+flag_sets = [int(x) for x in a.ab.split(",")] if a.ab else [0]
 out = torch.empty((a.height, a.width, 4), dtype=torch.float32, device="cuda")
 tiles = [(0, 0, a.width, a.height)]
+res = {f: [] for f in flag_sets}
+imgs = {}
 for r in range(a.reps):
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    st = hrt.render_tiles_device(s, cam, p, tiles, out.data_ptr(), 0, want_stats=True)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    print(f"rep {r}: {dt*1e3:.1f} ms  segments {st.segments}  seg/sample {st.segments/st.samples:.3f}  "
-          f"{st.segments/dt/1e6:.1f} Mrays/s  {st.samples/dt/1e6:.1f} Msamples/s", flush=True)
+    for fl in flag_sets:
+        p = hrt.params(a.width, a.height, a.spp, a.depth, 1, tuple(s.info.background), flags=fl)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        st = hrt.render_tiles_device(s, cam, p, tiles, out.data_ptr(), 0, want_stats=True)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        res[fl].append(st.segments / dt / 1e6)
+        imgs[fl] = out.clone()
+        print(f"rep {r} flags {fl}: {dt*1e3:.1f} ms  segments {st.segments}  seg/sample {st.segments/st.samples:.3f}  "
+              f"{st.segments/dt/1e6:.1f} Mrays/s  {st.samples/dt/1e6:.1f} Msamples/s", flush=True)
+for fl in flag_sets:
+    print(f"flags {fl}: median {sorted(res[fl])[len(res[fl])//2]:.1f} Mrays/s  identical-to-first {bool(torch.equal(imgs[fl], imgs[flag_sets[0]]))}")
 img = out.cpu().numpy()
 print("mean rgb", img[..., :3].mean(axis=(0, 1)), "finite", bool(np.isfinite(img).all()))
