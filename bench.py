@@ -202,7 +202,7 @@ def main():
                 "rays_per_sample": round(seg_all / max(1.0, samples_all), 4),
                 "msamples_per_s": round(samples_all * args.steps / dt / 1e6, 2),
                 "parallelism": f"{world} GPU(s), {args.scaling} split, no collectives",
-                "cull_mode": "slab" if si.cull_mode == 1 else "reference",
+                "cull_mode": {0: "reference", 1: "slab (approximate)", 2: "exact (reference test + provably safe culling)"}[si.cull_mode],
             },
             "roofline": roofline,
             "cpu_baseline": cpu,

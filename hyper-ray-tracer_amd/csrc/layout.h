@@ -29,8 +29,10 @@ enum : uint32_t {
   K_PRIM = 2,       /* primitive without box (List / Cuboid side / root) */
   K_INST_BEGIN = 3, /* Translation / Rotation: transform ray (payload = inst) */
   K_INST_END = 4,   /* restore ray */
-  K_MEDIUM = 5      /* ConstantMedium (payload = medium) */
+  K_MEDIUM = 5,     /* ConstantMedium (payload = medium) */
+  K_BOX_LEAF = 6    /* SAH stream leaf: box, then prims [start, start+count) (payload = start | (count-1) << 21) */
 };
+constexpr uint32_t LEAF_MAX = 4; /* primitives per SAH leaf */
 struct alignas(16) Node {
   float mn[3];
   uint32_t skip;
@@ -125,8 +127,20 @@ constexpr uint32_t F_BASIC = F_MOVING | F_CHECKER | F_METAL | F_DIELECTRIC;
 /* box-culling modes */
 enum : int {
   CULL_REFERENCE = 0, /* aabb.rs:20-47 verbatim: each axis tested alone against [t_min, t_max] */
-  CULL_SLAB = 1       /* intervals narrowed across axes (a subset of the reference's passes) */
+  CULL_SLAB = 1,      /* intervals narrowed across axes: fast, NOT bit-faithful (f32 grazing hits) */
+  CULL_EXACT = 2      /* the reference test, plus culling of boxes that no accepted hit can come
+                         from: the box inflated by EXACT_MARGIN x its distance misses the ray */
 };
+/* Bound on how far outside a primitive an f32 hit test of the reference can place an ACCEPTED hit,
+ * relative to the distance |oc| from the ray origin: the sphere discriminant's rounding error lets a
+ * grazing ray "hit" up to sqrt(32 eps) |oc| (~1.4e-3 |oc|) away from the sphere (sphere.rs:42-46);
+ * rect and box arithmetic err by ~1e-7 relative.  The box's L-inf distance D bounds |oc| / sqrt(3).
+ * 4e-3 * D covers sqrt(3) * 1.4e-3 * D with a 1.65x margin. */
+constexpr float EXACT_MARGIN = 4.0e-3f;
+/* Node.kp bit 31: the node's reference box may not contain its geometry (a ZX rect, rect.rs:97-102,
+ * below it): only the reference test may cull it. */
+constexpr uint32_t NODE_REF_ONLY = 1u << 31;
+constexpr uint32_t KIND_MASK = 0x7Fu;
 
 }  // namespace gpu
 }  // namespace hrt

@@ -67,6 +67,8 @@ struct KParams {
   /* sample chunks: a work item is (pixel, chunk of `chunk` consecutive samples) */
   uint32_t chunk, n_chunks, n_out;
   uint32_t n_prims;
+  uint32_t n_nodes;    /* node-stream entries to stage in LDS */
+  uint32_t stream_len; /* FAST: length of one octant stream */
   float4* partial; /* [n_chunks][n_out] chunk sums (n_chunks > 1) */
 };
 
@@ -92,12 +94,40 @@ __device__ __forceinline__ void set_ray(TRay& r, Vec3 o, Vec3 d, float time) {
 
 __device__ __forceinline__ float4 ld4(const void* p) { return *reinterpret_cast<const float4*>(p); }
 
-/* aabb.rs:20-47 (CULL_REFERENCE) or its narrowed form (CULL_SLAB) */
+/* aabb.rs:20-47 (CULL_REFERENCE), its narrowed form (CULL_SLAB), or CULL_EXACT: the reference test
+ * AND an inflated slab test that only rejects boxes no accepted hit can come from (layout.h). */
 template <int CULL>
 __device__ __forceinline__ bool box_hit(const float4& a, const float4& b, const TRay& r, float tmin,
-                                        float tmax) {
+                                        float tmax, bool ref_only = false) {
   const float mn[3] = {a.x, a.y, a.z}, mx[3] = {b.x, b.y, b.z};
   const float o[3] = {r.o.x, r.o.y, r.o.z}, inv[3] = {r.inv.x, r.inv.y, r.inv.z};
+  if (CULL == G::CULL_EXACT) {
+    float dmn[3], dmx[3];
+    float dist = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      dmn[k] = mn[k] - o[k];
+      dmx[k] = mx[k] - o[k];
+      dist = fmaxf(dist, fmaxf(fabsf(dmn[k]), fabsf(dmx[k])));
+    }
+    const float margin = G::EXACT_MARGIN * dist;
+    bool ok = true;
+    float lo = tmin, hi = tmax;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      float ts = dmn[k] * inv[k];
+      float te = dmx[k] * inv[k];
+      if (inv[k] < 0.0f) { float t = ts; ts = te; te = t; }
+      float l1 = ts > tmin ? ts : tmin;
+      float h1 = te < tmax ? te : tmax;
+      ok = ok & !(h1 <= l1);
+      const float w = margin * fabsf(inv[k]);
+      const float ts2 = ts - w, te2 = te + w;
+      lo = ts2 > lo ? ts2 : lo;
+      hi = te2 < hi ? te2 : hi;
+    }
+    return ok & (ref_only | !(hi < lo));
+  }
   if (CULL == G::CULL_REFERENCE) {
     bool ok = true;
 #pragma unroll
@@ -198,12 +228,17 @@ struct PathKey {
 /* The world walk.  Closest hit over [begin, end) of the node stream with t in [tmin, closest]:
  * `winner` = node index of the accepted leaf (NONE if nothing).  MEDIA: ConstantMedium nodes are
  * evaluated (their boundary walks are nested calls with MEDIA = false). */
-template <int CULL, bool FULL, bool MEDIA, bool COUNT>
+template <int CULL, bool FULL, bool MEDIA, bool COUNT, bool FAST = false>
 __device__ void trace(const KParams& P, const G::Node* __restrict__ nodes, const G::Prim* __restrict__ prims,
                       uint32_t begin, uint32_t end, Vec3 o, Vec3 d, float time, float tmin, float& closest,
                       uint32_t& winner, const PathKey& pk, Counts& cn) {
   TRay r;
   set_ray(r, o, d, time);
+  if constexpr (FAST) { /* the stream whose near-child order matches the ray's direction octant */
+    const uint32_t oct = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+    begin = oct * P.stream_len;
+    end = begin + P.stream_len;
+  }
   Vec3 so[G::MAX_INST_DEPTH], sd[G::MAX_INST_DEPTH];
   int sp = 0;
   uint32_t i = begin;
@@ -212,12 +247,34 @@ __device__ void trace(const KParams& P, const G::Node* __restrict__ nodes, const
     const float4 a = ld4(np->mn);
     const float4 b = ld4(np->mx);
     const uint32_t kp = __float_as_uint(b.w);
-    const uint32_t kind = kp >> 24;
+    const uint32_t kind = (kp >> 24) & G::KIND_MASK;
+    const bool ref_only = (kp & G::NODE_REF_ONLY) != 0;
     const uint32_t payload = kp & 0xFFFFFFu;
     const uint32_t here = i;
     if constexpr (COUNT) cn.nodes++;
-    if (kind <= G::K_BOX_PRIM) {
+    if constexpr (FAST) {
       bool pass = box_hit<CULL>(a, b, r, tmin, closest);
+      if (kind == G::K_BOX) {
+        i = pass ? i + 1 : __float_as_uint(a.w);
+        continue;
+      }
+      i++;
+      if (!pass) continue;
+      /* K_BOX_LEAF: up to LEAF_MAX primitives, tested in order */
+      const uint32_t start = payload & 0x1FFFFFu, cnt = (payload >> 21) + 1u;
+      for (uint32_t k = 0; k < cnt; k++) {
+        const G::Prim* pp = prims + start + k;
+        if constexpr (COUNT) cn.prims++;
+        float t;
+        if (sphere_root(pp, pp->km & 3u, r, tmin, closest, t)) {
+          closest = t;
+          winner = start + k;
+        }
+      }
+      continue;
+    }
+    if (kind <= G::K_BOX_PRIM) {
+      bool pass = box_hit<CULL>(a, b, r, tmin, closest, ref_only);
       if (kind == G::K_BOX) {
         i = pass ? i + 1 : __float_as_uint(a.w);
         continue;
@@ -278,7 +335,7 @@ __device__ void trace(const KParams& P, const G::Node* __restrict__ nodes, const
     else h = sphere_root(pp, pkind, r, tmin, closest, t);
     if (h) {
       closest = t;
-      winner = here;
+      winner = FULL ? here : payload; /* BASIC kernels name the primitive directly */
     }
   }
 }
@@ -308,14 +365,11 @@ __device__ __forceinline__ void sphere_uv(Vec3 p, float& u, float& v) {
  * constant_medium.rs:66-75, then translation.rs:33-35 / rotation.rs:119-132 on the way out). */
 template <bool FULL>
 __device__ Rec make_record(const KParams& P, uint32_t winner, float t, Vec3 wo, Vec3 wd, float time) {
-  const G::Node* np = P.nodes + winner;
-  const uint32_t kp = np->kp;
-  const uint32_t kind = kp >> 24, payload = kp & 0xFFFFFFu;
   Rec rec;
   rec.u = 0.0f;
   rec.v = 0.0f;
-  if constexpr (!FULL) {
-    const G::Prim* pp = P.prims + payload;
+  if constexpr (!FULL) { /* winner is the primitive index */
+    const G::Prim* pp = P.prims + winner;
     const uint32_t km = pp->km;
     float4 p0 = ld4(pp->p0);
     Vec3 c = v3(p0.x, p0.y, p0.z);
@@ -330,6 +384,9 @@ __device__ Rec make_record(const KParams& P, uint32_t winner, float t, Vec3 wo, 
     set_face_normal(rec, wd, outward);
     return rec;
   } else {
+    const G::Node* np = P.nodes + winner;
+    const uint32_t kp = np->kp;
+    const uint32_t kind = (kp >> 24) & G::KIND_MASK, payload = kp & 0xFFFFFFu;
     uint32_t parent;
     if (kind == G::K_MEDIUM) parent = P.media[payload].parent;
     else parent = P.prims[payload].parent;
@@ -470,16 +527,135 @@ __device__ Vec3 tex_value(const KParams& P, uint32_t id, float u, float v, Vec3 
   return v3(0.0f, 0.0f, 0.0f);
 }
 
+/* ------------------------------------------------------------------ one path, one segment at a time */
+struct PathState {
+  Rng rng;
+  PathKey pk;
+  uint32_t depth_left;
+  Vec3 ro, rd;
+  float rtime;
+  Vec3 thr, rad;
+  bool traced; /* the last segment() call made a world.hit call */
+};
+
+/* application.rs:444-447 + camera.rs:85-95: jitter, lens sample, shutter time */
+__device__ __forceinline__ void start_sample(const KParams& P, PathState& ps, uint32_t px, uint32_t py,
+                                             uint32_t sample) {
+  ps.pk.pkey = path_key(P.seed, py * P.W + px, P.sample_offset + sample);
+  ps.pk.segment = 0;
+  ps.rng = rng_from_key(ps.pk.pkey);
+  float u = ((float)px + ps.rng.gen_f32()) / ((float)P.W - 1.0f);
+  float v = ((float)py + ps.rng.gen_f32()) / ((float)P.H - 1.0f);
+  Vec3 disk = random_in_unit_disk(ps.rng);
+  ps.rtime = ps.rng.gen_range_f32(P.time0, P.time1);
+  Vec3 rdk = P.lens_radius * disk;
+  Vec3 offset = P.cam_u * rdk.x + P.cam_vv * rdk.y;
+  ps.ro = P.cam_origin + offset;
+  ps.rd = (((P.cam_llc + u * P.cam_h) + v * P.cam_v) - P.cam_origin) - offset;
+  ps.thr = v3(1.0f, 1.0f, 1.0f);
+  ps.rad = v3(0.0f, 0.0f, 0.0f);
+  ps.depth_left = P.max_depth;
+}
+
+/* One step of ray_color (application.rs:477-495).  Returns true when the path is finished.
+ * dbg (debug kernel only): receives o, d, time, t, winner of the traced segment. */
+template <int CULL, bool FULL, bool COUNT, bool FAST>
+__device__ __forceinline__ bool segment(const KParams& P, const G::Node* nodes, const G::Prim* prims,
+                                        PathState& ps, Counts& cn, float* dbg) {
+  ps.traced = false;
+  if (ps.depth_left == 0) return true; /* depth cap: black (:478-480) */
+  float closest = __uint_as_float(0x7f800000u);
+  uint32_t winner = G::NONE;
+  trace<CULL, FULL, FULL, COUNT, FAST>(P, nodes, prims, 0u, P.main_end, ps.ro, ps.rd, ps.rtime, P.t_min, closest,
+                                       winner, ps.pk, cn);
+  ps.traced = true;
+  ps.pk.segment++;
+  if (dbg) {
+    dbg[0] = ps.ro.x; dbg[1] = ps.ro.y; dbg[2] = ps.ro.z;
+    dbg[3] = ps.rd.x; dbg[4] = ps.rd.y; dbg[5] = ps.rd.z;
+    dbg[6] = ps.rtime; dbg[7] = closest; dbg[8] = __uint_as_float(winner);
+  }
+  if (winner == G::NONE) {
+    ps.rad = ps.rad + mul_elem(ps.thr, P.background);
+    return true;
+  }
+  Rec rec = make_record<FULL>(P, winner, closest, ps.ro, ps.rd, ps.rtime);
+  const G::Mat M = P.mats[rec.mat];
+  Vec3 emitted = v3(0.0f, 0.0f, 0.0f);
+  Vec3 att = v3(0.0f, 0.0f, 0.0f), ndir = v3(0.0f, 0.0f, 0.0f);
+  bool scattered = false;
+  Rng& rng = ps.rng;
+  if (M.kind == G::M_LAMBERTIAN) { /* lambertian.rs:27-38 */
+    ndir = rec.n + random_unit_vector(rng);
+    if (near_zero(ndir)) ndir = rec.n;
+    att = tex_value<FULL, COUNT>(P, M.tex, rec.u, rec.v, rec.p, cn);
+    scattered = true;
+  } else if (M.kind == G::M_METAL) { /* metal.rs:29-42 */
+    Vec3 reflected = reflect(normalize(ps.rd), rec.n);
+    ndir = reflected + M.a[3] * random_in_unit_sphere(rng);
+    scattered = dot(ndir, rec.n) > 0.0f;
+    att = v3(M.a[0], M.a[1], M.a[2]);
+  } else if (M.kind == G::M_DIELECTRIC) { /* dielectric.rs:31-55 */
+    float ratio = rec.front ? (1.0f / M.a[0]) : M.a[0];
+    Vec3 ud = normalize(ps.rd);
+    float cos_theta = min_rs(dot(-ud, rec.n), 1.0f);
+    float sin_theta = sqrtf(1.0f - cos_theta * cos_theta);
+    bool cannot_refract = (ratio * sin_theta) > 1.0f;
+    if (cannot_refract || reflectance(cos_theta, ratio) > rng.gen_f32()) ndir = reflect(ud, rec.n);
+    else ndir = refract(ud, rec.n, ratio);
+    att = v3(1.0f, 1.0f, 1.0f);
+    scattered = true;
+  } else if (FULL && M.kind == G::M_DIFFUSE_LIGHT) { /* diffuse_light.rs:20-28 */
+    emitted = tex_value<FULL, COUNT>(P, M.tex, rec.u, rec.v, rec.p, cn);
+  } else if (FULL && M.kind == G::M_ISOTROPIC) { /* isotropic.rs:26-33 */
+    att = tex_value<FULL, COUNT>(P, M.tex, rec.u, rec.v, rec.p, cn);
+    ndir = random_in_unit_sphere(rng);
+    scattered = true;
+  }
+  /* L = emitted + att * L_next, accumulated front to back */
+  ps.rad = ps.rad + mul_elem(ps.thr, emitted);
+  if (!scattered) return true;
+  ps.thr = mul_elem(ps.thr, att);
+  ps.ro = rec.p;
+  ps.rd = ndir;
+  ps.depth_left--;
+  return false;
+}
+
+/* Diagnostics: trace ONE path (pixel, sample) and record every segment (9 floats each). */
+template <int CULL, bool FULL, bool FAST>
+__global__ void debug_path_kernel(KParams P, uint32_t px, uint32_t py, uint32_t sample, float* out,
+                                  uint32_t max_seg, uint32_t* n_out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  PathState ps;
+  Counts cn{0u, 0u, 0u};
+  start_sample(P, ps, px, py, sample);
+  uint32_t n = 0;
+  float scratch[9];
+  for (;;) {
+    bool done = segment<CULL, FULL, false, FAST>(P, P.nodes, P.prims, ps, cn, n < max_seg ? out + 9 * n : scratch);
+    if (ps.traced) n++;
+    if (done) break;
+  }
+  *n_out = n;
+  out[9 * max_seg + 0] = ps.rad.x;
+  out[9 * max_seg + 1] = ps.rad.y;
+  out[9 * max_seg + 2] = ps.rad.z;
+}
+
 /* ------------------------------------------------------------------ the megakernel */
 /* LDS: the node stream and primitive records are copied into LDS once per workgroup (they are
  * read ~60 times per ray by dependent loads; LDS latency is a fraction of an L2 hit). */
-template <int CULL, bool FULL, bool COUNT, bool LDS>
-__global__ __launch_bounds__(LDS ? 512 : 256) void render_kernel(KParams P) {
+template <bool LDS, bool FAST>
+constexpr int block_threads() { return LDS ? (FAST ? 1024 : 512) : 256; }
+
+template <int CULL, bool FULL, bool COUNT, bool LDS, bool FAST>
+__global__ __launch_bounds__((block_threads<LDS, FAST>())) void render_kernel(KParams P) {
   extern __shared__ float4 lds_scene[];
   const G::Node* nodes = P.nodes;
   const G::Prim* prims = P.prims;
   if constexpr (LDS) {
-    const uint32_t n4 = P.main_end * (uint32_t)(sizeof(G::Node) / 16);
+    const uint32_t n4 = P.n_nodes * (uint32_t)(sizeof(G::Node) / 16);
     const uint32_t p4 = P.n_prims * (uint32_t)(sizeof(G::Prim) / 16);
     const float4* gn = reinterpret_cast<const float4*>(P.nodes);
     const float4* gp = reinterpret_cast<const float4*>(P.prims);
@@ -491,18 +667,20 @@ __global__ __launch_bounds__(LDS ? 512 : 256) void render_kernel(KParams P) {
   }
   const uint32_t lane = threadIdx.x & 63u;
   const float scale = 1.0f / (float)P.spp; /* application.rs:403 */
-  const float inf = __uint_as_float(0x7f800000u);
 
   bool has_item = false, exhausted = false, in_path = false;
   uint32_t px = 0, py = 0, out_idx = 0, chunk = 0, sample = 0, sample_end = 0;
   Vec3 sum = v3(0.0f, 0.0f, 0.0f);
-  Rng rng;
-  rng.s0 = rng.s1 = rng.s2 = rng.s3 = 1u;
-  PathKey pk{0ull, 0u};
-  uint32_t depth_left = 0;
-  Vec3 ro = v3(0.0f, 0.0f, 0.0f), rd = v3(0.0f, 0.0f, 1.0f);
-  float rtime = 0.0f;
-  Vec3 thr = v3(1.0f, 1.0f, 1.0f), rad = v3(0.0f, 0.0f, 0.0f);
+  PathState ps;
+  ps.rng.s0 = ps.rng.s1 = ps.rng.s2 = ps.rng.s3 = 1u;
+  ps.pk = PathKey{0ull, 0u};
+  ps.depth_left = 0;
+  ps.ro = v3(0.0f, 0.0f, 0.0f);
+  ps.rd = v3(0.0f, 0.0f, 1.0f);
+  ps.rtime = 0.0f;
+  ps.thr = v3(1.0f, 1.0f, 1.0f);
+  ps.rad = v3(0.0f, 0.0f, 0.0f);
+  ps.traced = false;
   uint32_t n_seg = 0, n_samples = 0, n_pixels = 0;
   Counts cn{0u, 0u, 0u};
 
@@ -550,85 +728,14 @@ __global__ __launch_bounds__(LDS ? 512 : 256) void render_kernel(KParams P) {
     if (!__any(has_item || !exhausted)) break;
     if (!has_item) continue;
 
-    /* ---- start the next sample (application.rs:444-447, camera.rs:85-95) ---- */
     if (!in_path) {
-      pk.pkey = path_key(P.seed, py * P.W + px, P.sample_offset + sample);
-      pk.segment = 0;
-      rng = rng_from_key(pk.pkey);
-      float u = ((float)px + rng.gen_f32()) / ((float)P.W - 1.0f);
-      float v = ((float)py + rng.gen_f32()) / ((float)P.H - 1.0f);
-      Vec3 disk = random_in_unit_disk(rng);
-      rtime = rng.gen_range_f32(P.time0, P.time1);
-      Vec3 rdk = P.lens_radius * disk;
-      Vec3 offset = P.cam_u * rdk.x + P.cam_vv * rdk.y;
-      ro = P.cam_origin + offset;
-      rd = (((P.cam_llc + u * P.cam_h) + v * P.cam_v) - P.cam_origin) - offset;
-      thr = v3(1.0f, 1.0f, 1.0f);
-      rad = v3(0.0f, 0.0f, 0.0f);
-      depth_left = P.max_depth;
+      start_sample(P, ps, px, py, sample);
       in_path = true;
     }
-
-    /* ---- one segment of ray_color (application.rs:477-495) ---- */
-    bool done = false;
-    if (depth_left == 0) {
-      done = true; /* depth cap: black (:478-480) */
-    } else {
-      float closest = inf;
-      uint32_t winner = G::NONE;
-      trace<CULL, FULL, FULL, COUNT>(P, nodes, prims, 0u, P.main_end, ro, rd, rtime, P.t_min, closest, winner, pk, cn);
-      n_seg++;
-      pk.segment++;
-      if (winner == G::NONE) {
-        rad = rad + mul_elem(thr, P.background);
-        done = true;
-      } else {
-        Rec rec = make_record<FULL>(P, winner, closest, ro, rd, rtime);
-        const G::Mat M = P.mats[rec.mat];
-        Vec3 emitted = v3(0.0f, 0.0f, 0.0f);
-        Vec3 att = v3(0.0f, 0.0f, 0.0f), ndir = v3(0.0f, 0.0f, 0.0f);
-        bool scattered = false;
-        if (M.kind == G::M_LAMBERTIAN) { /* lambertian.rs:27-38 */
-          ndir = rec.n + random_unit_vector(rng);
-          if (near_zero(ndir)) ndir = rec.n;
-          att = tex_value<FULL, COUNT>(P, M.tex, rec.u, rec.v, rec.p, cn);
-          scattered = true;
-        } else if (M.kind == G::M_METAL) { /* metal.rs:29-42 */
-          Vec3 reflected = reflect(normalize(rd), rec.n);
-          ndir = reflected + M.a[3] * random_in_unit_sphere(rng);
-          scattered = dot(ndir, rec.n) > 0.0f;
-          att = v3(M.a[0], M.a[1], M.a[2]);
-        } else if (M.kind == G::M_DIELECTRIC) { /* dielectric.rs:31-55 */
-          float ratio = rec.front ? (1.0f / M.a[0]) : M.a[0];
-          Vec3 ud = normalize(rd);
-          float cos_theta = min_rs(dot(-ud, rec.n), 1.0f);
-          float sin_theta = sqrtf(1.0f - cos_theta * cos_theta);
-          bool cannot_refract = (ratio * sin_theta) > 1.0f;
-          if (cannot_refract || reflectance(cos_theta, ratio) > rng.gen_f32()) ndir = reflect(ud, rec.n);
-          else ndir = refract(ud, rec.n, ratio);
-          att = v3(1.0f, 1.0f, 1.0f);
-          scattered = true;
-        } else if (FULL && M.kind == G::M_DIFFUSE_LIGHT) { /* diffuse_light.rs:20-28 */
-          emitted = tex_value<FULL, COUNT>(P, M.tex, rec.u, rec.v, rec.p, cn);
-        } else if (FULL && M.kind == G::M_ISOTROPIC) { /* isotropic.rs:26-33 */
-          att = tex_value<FULL, COUNT>(P, M.tex, rec.u, rec.v, rec.p, cn);
-          ndir = random_in_unit_sphere(rng);
-          scattered = true;
-        }
-        /* L = emitted + att * L_next, accumulated front to back */
-        rad = rad + mul_elem(thr, emitted);
-        if (scattered) {
-          thr = mul_elem(thr, att);
-          ro = rec.p;
-          rd = ndir;
-          depth_left--;
-        } else {
-          done = true;
-        }
-      }
-    }
+    const bool done = segment<CULL, FULL, COUNT, FAST>(P, nodes, prims, ps, cn, nullptr);
+    if (ps.traced) n_seg++;
     if (done) {
-      sum = sum + rad; /* application.rs:448, samples of a chunk in order */
+      sum = sum + ps.rad; /* application.rs:448, samples of a chunk in order */
       in_path = false;
       n_samples++;
       if (++sample == sample_end) {
@@ -725,13 +832,13 @@ hrt_status hguard(F&& f) {
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-template <int CULL, bool FULL, bool COUNT, bool LDS>
+template <int CULL, bool FULL, bool COUNT, bool LDS, bool FAST>
 int resident_grid(int device, size_t smem) {
   static int cached[64] = {0};
   static size_t cached_smem[64] = {0};
   if (device >= 0 && device < 64 && cached[device] && cached_smem[device] == smem) return cached[device];
-  auto fn = render_kernel<CULL, FULL, COUNT, LDS>;
-  const int block = LDS ? 512 : 256;
+  auto fn = render_kernel<CULL, FULL, COUNT, LDS, FAST>;
+  const int block = block_threads<LDS, FAST>();
   if (LDS) hip_check(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem),
                      "hipFuncSetAttribute(LDS)");
   int per_cu = 0;
@@ -744,36 +851,100 @@ int resident_grid(int device, size_t smem) {
   return g;
 }
 
-template <int CULL, bool FULL, bool COUNT, bool LDS>
+template <int CULL, bool FULL, bool COUNT, bool LDS, bool FAST>
 void launch(const KParams& kp, int device, hipStream_t stream, size_t smem) {
-  int grid = resident_grid<CULL, FULL, COUNT, LDS>(device, smem);
-  hipLaunchKernelGGL((render_kernel<CULL, FULL, COUNT, LDS>), dim3(grid), dim3(LDS ? 512 : 256), LDS ? smem : 0,
-                     stream, kp);
+  int grid = resident_grid<CULL, FULL, COUNT, LDS, FAST>(device, smem);
+  hipLaunchKernelGGL((render_kernel<CULL, FULL, COUNT, LDS, FAST>), dim3(grid), dim3(block_threads<LDS, FAST>()),
+                     LDS ? smem : 0, stream, kp);
   hip_check(hipGetLastError(), "render_kernel launch");
 }
 
-/* LDS residency: the traversed node stream + primitives must fit twice per CU (two 512-thread
- * workgroups, 160 KiB LDS per CU). */
+/* LDS residency: the reference-order stream must fit twice per CU (two 512-thread workgroups of the
+ * 160 KiB), the 8 SAH octant streams once (one 1024-thread workgroup). */
 constexpr size_t LDS_SCENE_MAX = 72 * 1024;
+constexpr size_t LDS_FAST_MAX = 150 * 1024;
 
-size_t lds_bytes(const hrt_scene* s) {
-  return s->main_end * sizeof(G::Node) + s->g_prims.size() * sizeof(G::Prim);
+struct Plan {
+  bool full, fast, lds;
+  int cull;
+  size_t smem;
+};
+
+Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
+  Plan pl;
+  pl.full = (s->feature_mask & ~G::F_BASIC) != 0;
+  /* default: exact.  A ray time outside the interval the BVH boxes were built for can put a moving
+   * sphere outside its box: only the reference test is then faithful. */
+  const bool shutter_ok = cam->time0 >= s->box_t0 && cam->time1 <= s->box_t1;
+  pl.cull = s->cull_mode;
+  if ((flags & HRT_RENDER_FAST_CULL) && s->all_boxes_ok && shutter_ok) pl.cull = G::CULL_SLAB;
+  if ((flags & HRT_RENDER_REFERENCE_CULL) || !shutter_ok) pl.cull = G::CULL_REFERENCE;
+  /* SAH streams: opt-in approximate mode for sphere-only scenes (boxes over t in [0, 1]) */
+  pl.fast = !pl.full && pl.cull == G::CULL_SLAB && s->f_stream_len > 0 && (flags & HRT_RENDER_SAH) != 0 &&
+            cam->time0 >= 0.0f && cam->time1 <= 1.0f;
+  pl.smem = pl.fast ? (8 * (size_t)s->f_stream_len * sizeof(G::Node) + s->f_prims.size() * sizeof(G::Prim))
+                    : (s->main_end * sizeof(G::Node) + s->g_prims.size() * sizeof(G::Prim));
+  pl.lds = (flags & HRT_RENDER_NO_LDS) == 0 && !pl.full && pl.smem <= (pl.fast ? LDS_FAST_MAX : LDS_SCENE_MAX);
+  return pl;
 }
 
 template <bool COUNT>
-void launch_any(const hrt_scene* s, const KParams& kp, hipStream_t stream, bool allow_lds) {
-  const bool full = (s->feature_mask & ~G::F_BASIC) != 0;
-  const size_t smem = lds_bytes(s);
-  const bool lds = allow_lds && !full && smem <= LDS_SCENE_MAX;
-  if (s->cull_mode == G::CULL_SLAB) {
-    if (full) launch<G::CULL_SLAB, true, COUNT, false>(kp, s->device, stream, 0);
-    else if (lds) launch<G::CULL_SLAB, false, COUNT, true>(kp, s->device, stream, smem);
-    else launch<G::CULL_SLAB, false, COUNT, false>(kp, s->device, stream, 0);
+void launch_any(const hrt_scene* s, const Plan& pl, const KParams& kp, hipStream_t stream) {
+  const size_t smem = pl.lds ? pl.smem : 0;
+  if (pl.fast) {
+    if (pl.lds) launch<G::CULL_SLAB, false, COUNT, true, true>(kp, s->device, stream, smem);
+    else launch<G::CULL_SLAB, false, COUNT, false, true>(kp, s->device, stream, 0);
+  } else if (pl.cull == G::CULL_EXACT) {
+    if (pl.full) launch<G::CULL_EXACT, true, COUNT, false, false>(kp, s->device, stream, 0);
+    else if (pl.lds) launch<G::CULL_EXACT, false, COUNT, true, false>(kp, s->device, stream, smem);
+    else launch<G::CULL_EXACT, false, COUNT, false, false>(kp, s->device, stream, 0);
+  } else if (pl.cull == G::CULL_SLAB) {
+    if (pl.full) launch<G::CULL_SLAB, true, COUNT, false, false>(kp, s->device, stream, 0);
+    else if (pl.lds) launch<G::CULL_SLAB, false, COUNT, true, false>(kp, s->device, stream, smem);
+    else launch<G::CULL_SLAB, false, COUNT, false, false>(kp, s->device, stream, 0);
   } else {
-    if (full) launch<G::CULL_REFERENCE, true, COUNT, false>(kp, s->device, stream, 0);
-    else if (lds) launch<G::CULL_REFERENCE, false, COUNT, true>(kp, s->device, stream, smem);
-    else launch<G::CULL_REFERENCE, false, COUNT, false>(kp, s->device, stream, 0);
+    if (pl.full) launch<G::CULL_REFERENCE, true, COUNT, false, false>(kp, s->device, stream, 0);
+    else if (pl.lds) launch<G::CULL_REFERENCE, false, COUNT, true, false>(kp, s->device, stream, smem);
+    else launch<G::CULL_REFERENCE, false, COUNT, false, false>(kp, s->device, stream, 0);
   }
+}
+
+/* scene + camera + render knobs of a launch (work-distribution fields are set by the caller) */
+KParams scene_params(const hrt_scene* s, const hrt_camera* cam, const hrt_render_params* p, const Plan& pl) {
+  KParams kp;
+  memset(&kp, 0, sizeof(kp));
+  uint8_t* base = (uint8_t*)s->d_blob;
+  kp.nodes = (const G::Node*)(base + (pl.fast ? s->off_fnodes : s->off_nodes));
+  kp.prims = (const G::Prim*)(base + (pl.fast ? s->off_fprims : s->off_prims));
+  kp.insts = (const G::Inst*)(base + s->off_insts);
+  kp.media = (const G::Medium*)(base + s->off_media);
+  kp.mats = (const G::Mat*)(base + s->off_mats);
+  kp.texs = (const G::Tex*)(base + s->off_texs);
+  kp.perlin = (const G::Perlin*)(base + s->off_perlin);
+  kp.images = (const uint8_t*)(base + s->off_images);
+  kp.main_end = s->main_end;
+  kp.ln_e = s->ln_e;
+  kp.cam_origin = v3(cam->origin[0], cam->origin[1], cam->origin[2]);
+  kp.cam_llc = v3(cam->lower_left_corner[0], cam->lower_left_corner[1], cam->lower_left_corner[2]);
+  kp.cam_h = v3(cam->horizontal[0], cam->horizontal[1], cam->horizontal[2]);
+  kp.cam_v = v3(cam->vertical[0], cam->vertical[1], cam->vertical[2]);
+  kp.cam_u = v3(cam->u[0], cam->u[1], cam->u[2]);
+  kp.cam_vv = v3(cam->v[0], cam->v[1], cam->v[2]);
+  kp.lens_radius = cam->lens_radius;
+  kp.time0 = cam->time0;
+  kp.time1 = cam->time1;
+  kp.W = p->width;
+  kp.H = p->height;
+  kp.spp = p->samples;
+  kp.max_depth = p->max_depth;
+  kp.sample_offset = p->sample_offset;
+  kp.t_min = p->t_min;
+  kp.background = v3(p->background[0], p->background[1], p->background[2]);
+  kp.seed = p->seed;
+  kp.n_nodes = pl.fast ? 8 * s->f_stream_len : s->main_end;
+  kp.n_prims = (uint32_t)(pl.fast ? s->f_prims.size() : s->g_prims.size());
+  kp.stream_len = pl.fast ? s->f_stream_len : 0;
+  return kp;
 }
 
 }  // namespace
@@ -800,6 +971,8 @@ hrt_status device_upload(hrt_scene* s, int device) {
     s->off_texs = section(s->g_texs.size() * sizeof(G::Tex));
     s->off_perlin = section(s->perlin.size() * sizeof(G::Perlin));
     s->off_images = section(s->images.size());
+    s->off_fnodes = section(s->f_nodes.size() * sizeof(G::Node));
+    s->off_fprims = section(s->f_prims.size() * sizeof(G::Prim));
     s->blob_bytes = off;
     std::vector<uint8_t> blob(off, 0);
     auto put = [&](size_t o, const void* src, size_t bytes) {
@@ -813,6 +986,8 @@ hrt_status device_upload(hrt_scene* s, int device) {
     put(s->off_texs, s->g_texs.data(), s->g_texs.size() * sizeof(G::Tex));
     put(s->off_perlin, s->perlin.data(), s->perlin.size() * sizeof(G::Perlin));
     put(s->off_images, s->images.data(), s->images.size());
+    put(s->off_fnodes, s->f_nodes.data(), s->f_nodes.size() * sizeof(G::Node));
+    put(s->off_fprims, s->f_prims.data(), s->f_prims.size() * sizeof(G::Prim));
     s->device = device; /* from here on device_release() cleans up whatever was allocated */
     hip_check(hipMalloc(&s->d_blob, off), "hipMalloc(scene)");
     hip_check(hipMemcpy(s->d_blob, blob.data(), off, hipMemcpyHostToDevice), "hipMemcpy(scene)");
@@ -861,7 +1036,8 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     if (!s || !cam || !p || !tiles || !d_rgba || n_tiles == 0)
       throw HipError{HRT_ERR_INVALID_ARG, "hrt_render_tiles_device: null argument"};
     if (!s->committed || !s->d_blob) throw HipError{HRT_ERR_STATE, "scene not committed"};
-    if (p->width < 2 || p->height < 2 || p->samples == 0 || (p->flags & ~(uint32_t)(HRT_RENDER_COUNT_WORK | HRT_RENDER_NO_LDS)) != 0)
+    if (p->width < 2 || p->height < 2 || p->samples == 0 || (p->flags & ~(uint32_t)(HRT_RENDER_COUNT_WORK | HRT_RENDER_NO_LDS | HRT_RENDER_REFERENCE_CULL |
+                                     HRT_RENDER_FAST_CULL | HRT_RENDER_SAH)) != 0)
       throw HipError{HRT_ERR_INVALID_ARG, "bad render params (width/height >= 2, samples > 0, known flags)"};
     if (!(cam->time0 < cam->time1)) throw HipError{HRT_ERR_INVALID_ARG, "camera time0 must be < time1"};
     /* sample chunks: spp <= 32 keeps one work item per pixel (the reference's sequential sum);
@@ -911,35 +1087,8 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     hip_check(hipMemsetAsync(scratch, 0, 64, stream), "hipMemsetAsync");
     hip_check(hipMemcpyAsync((uint8_t*)scratch + 64, (uint8_t*)sl.h_tiles + 64, tiles_bytes, hipMemcpyHostToDevice,
                              stream), "hipMemcpyAsync(tiles)");
-    KParams kp;
-    uint8_t* base = (uint8_t*)s->d_blob;
-    kp.nodes = (const G::Node*)(base + s->off_nodes);
-    kp.prims = (const G::Prim*)(base + s->off_prims);
-    kp.insts = (const G::Inst*)(base + s->off_insts);
-    kp.media = (const G::Medium*)(base + s->off_media);
-    kp.mats = (const G::Mat*)(base + s->off_mats);
-    kp.texs = (const G::Tex*)(base + s->off_texs);
-    kp.perlin = (const G::Perlin*)(base + s->off_perlin);
-    kp.images = (const uint8_t*)(base + s->off_images);
-    kp.main_end = s->main_end;
-    kp.ln_e = s->ln_e;
-    kp.cam_origin = v3(cam->origin[0], cam->origin[1], cam->origin[2]);
-    kp.cam_llc = v3(cam->lower_left_corner[0], cam->lower_left_corner[1], cam->lower_left_corner[2]);
-    kp.cam_h = v3(cam->horizontal[0], cam->horizontal[1], cam->horizontal[2]);
-    kp.cam_v = v3(cam->vertical[0], cam->vertical[1], cam->vertical[2]);
-    kp.cam_u = v3(cam->u[0], cam->u[1], cam->u[2]);
-    kp.cam_vv = v3(cam->v[0], cam->v[1], cam->v[2]);
-    kp.lens_radius = cam->lens_radius;
-    kp.time0 = cam->time0;
-    kp.time1 = cam->time1;
-    kp.W = p->width;
-    kp.H = p->height;
-    kp.spp = p->samples;
-    kp.max_depth = p->max_depth;
-    kp.sample_offset = p->sample_offset;
-    kp.t_min = p->t_min;
-    kp.background = v3(p->background[0], p->background[1], p->background[2]);
-    kp.seed = p->seed;
+    const Plan pl = plan(s, cam, p->flags);
+    KParams kp = scene_params(s, cam, p, pl);
     kp.tiles = (const G::TileDev*)((uint8_t*)scratch + 64);
     kp.n_tiles = n_tiles;
     kp.total_work = (uint32_t)pad;
@@ -950,10 +1099,8 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     kp.n_chunks = n_chunks;
     kp.n_out = (uint32_t)outp;
     kp.partial = (float4*)sl.d_partial;
-    kp.n_prims = (uint32_t)s->g_prims.size();
-    const bool allow_lds = (p->flags & HRT_RENDER_NO_LDS) == 0;
-    if (p->flags & HRT_RENDER_COUNT_WORK) launch_any<true>(s, kp, stream, allow_lds);
-    else launch_any<false>(s, kp, stream, allow_lds);
+    if (p->flags & HRT_RENDER_COUNT_WORK) launch_any<true>(s, pl, kp, stream);
+    else launch_any<false>(s, pl, kp, stream);
     if (n_chunks > 1) {
       uint32_t blocks = (uint32_t)std::min<uint64_t>((outp + 255) / 256, 4096);
       hipLaunchKernelGGL(reduce_chunks, dim3(blocks), dim3(256), 0, stream, (const float4*)sl.d_partial,
@@ -1011,6 +1158,36 @@ hrt_status hrt_render(hrt_scene* s, const hrt_camera* cam, const hrt_render_para
     if (prev >= 0) (void)hipSetDevice(prev);
   }
   return st;
+}
+
+hrt_status hrt_debug_trace_path(hrt_scene* s, const hrt_camera* cam, const hrt_render_params* p, uint32_t x,
+                                uint32_t y, uint32_t sample, uint32_t max_segments, float* out, uint32_t* n_segments) {
+  return hguard([&] {
+    if (!s || !cam || !p || !out || !n_segments || max_segments == 0)
+      throw HipError{HRT_ERR_INVALID_ARG, "hrt_debug_trace_path: bad argument"};
+    if (!s->committed || !s->d_blob) throw HipError{HRT_ERR_STATE, "scene not committed"};
+    if (x >= p->width || y >= p->height) throw HipError{HRT_ERR_INVALID_ARG, "pixel outside the image"};
+    DeviceGuard dg(s->device);
+    const Plan pl = plan(s, cam, p->flags);
+    KParams kp = scene_params(s, cam, p, pl);
+    size_t bytes = (9 * (size_t)max_segments + 3) * sizeof(float);
+    float* d_out = nullptr;
+    uint32_t* d_n = nullptr;
+    hip_check(hipMalloc((void**)&d_out, bytes), "hipMalloc");
+    hip_check(hipMalloc((void**)&d_n, 4), "hipMalloc");
+    if (pl.fast) hipLaunchKernelGGL((debug_path_kernel<G::CULL_SLAB, false, true>), dim3(1), dim3(64), 0, 0, kp, x, y, sample, d_out, max_segments, d_n);
+    else if (pl.full && pl.cull == G::CULL_EXACT) hipLaunchKernelGGL((debug_path_kernel<G::CULL_EXACT, true, false>), dim3(1), dim3(64), 0, 0, kp, x, y, sample, d_out, max_segments, d_n);
+    else if (pl.cull == G::CULL_EXACT) hipLaunchKernelGGL((debug_path_kernel<G::CULL_EXACT, false, false>), dim3(1), dim3(64), 0, 0, kp, x, y, sample, d_out, max_segments, d_n);
+    else if (pl.full && pl.cull == G::CULL_SLAB) hipLaunchKernelGGL((debug_path_kernel<G::CULL_SLAB, true, false>), dim3(1), dim3(64), 0, 0, kp, x, y, sample, d_out, max_segments, d_n);
+    else if (pl.full) hipLaunchKernelGGL((debug_path_kernel<G::CULL_REFERENCE, true, false>), dim3(1), dim3(64), 0, 0, kp, x, y, sample, d_out, max_segments, d_n);
+    else if (pl.cull == G::CULL_SLAB) hipLaunchKernelGGL((debug_path_kernel<G::CULL_SLAB, false, false>), dim3(1), dim3(64), 0, 0, kp, x, y, sample, d_out, max_segments, d_n);
+    else hipLaunchKernelGGL((debug_path_kernel<G::CULL_REFERENCE, false, false>), dim3(1), dim3(64), 0, 0, kp, x, y, sample, d_out, max_segments, d_n);
+    hip_check(hipGetLastError(), "debug_path_kernel launch");
+    hip_check(hipMemcpy(out, d_out, bytes, hipMemcpyDeviceToHost), "hipMemcpy");
+    hip_check(hipMemcpy(n_segments, d_n, 4, hipMemcpyDeviceToHost), "hipMemcpy");
+    (void)hipFree(d_out);
+    (void)hipFree(d_n);
+  });
 }
 
 hrt_status hrt_debug_device_math(int32_t op, const float* x, const float* y, float* out, uint32_t n) {

@@ -165,6 +165,9 @@ uint32_t count(const hrt_scene* s, uint32_t id) {
  * latter (closest hits do not depend on it). */
 uint32_t build_bvh(hrt_scene* s, std::vector<uint32_t> objects, float t0, float t1) {
   need(!objects.empty(), HRT_ERR_EMPTY, "no elements in scene (BvhNode::new with no objects)");
+  /* moving-sphere boxes cover [t0, t1] only: remember the shutter every BVH box is valid for */
+  s->box_t0 = std::max(s->box_t0, t0);
+  s->box_t1 = std::min(s->box_t1, t1);
   float ranges[3];
   for (int a = 0; a < 3; a++) {
     float mn = 3.40282347e+38f, mx = -3.40282347e+38f;
@@ -210,6 +213,22 @@ uint32_t build_bvh(hrt_scene* s, std::vector<uint32_t> objects, float t0, float 
   n.children = {left, right};
   for (uint32_t c : n.children) s->nodes[c].owned = true;
   return push_node(s, std::move(n));
+}
+
+/* Does the reference bounding box of `id` contain its geometry?  Only a ZX rect with a0..a1 != b0..b1
+ * breaks this (rect.rs:97-102 vs :57), directly or through the boxes that enclose it. */
+bool box_ok(const hrt_scene* s, uint32_t id) {
+  const HNode& n = s->nodes[id];
+  switch (n.kind) {
+    case N_RECT:
+      return n.plane != HRT_PLANE_ZX || (n.a0 == n.b0 && n.a1 == n.b1);
+    case N_CUBOID: case N_SPHERE: case N_MOVING:
+      return true;
+    default:
+      for (uint32_t c : n.children)
+        if (!box_ok(s, c)) return false;
+      return true;
+  }
 }
 
 /* ------------------------------------------------------------------ lowering (commit) */
@@ -273,11 +292,15 @@ struct Flattener {
     const HNode& n = s->nodes[id];
     switch (n.kind) {
       case N_BVH: {
+        const bool ok = box_ok(s, id);
+        if (!ok) s->all_boxes_ok = false;
         if (n.children.size() == 1 && is_prim(s->nodes[n.children[0]].kind)) {
-          emit_node(G::K_BOX_PRIM, emit_prim(n.children[0], parent), &n.box);
+          uint32_t me = emit_node(G::K_BOX_PRIM, emit_prim(n.children[0], parent), &n.box);
+          if (!ok) s->g_nodes[me].kp |= G::NODE_REF_ONLY;
           return;
         }
         uint32_t me = emit_node(G::K_BOX, 0, &n.box);
+        if (!ok) s->g_nodes[me].kp |= G::NODE_REF_ONLY;
         for (uint32_t c : n.children) emit(c, parent);
         s->g_nodes[me].skip = (uint32_t)s->g_nodes.size();
         return;
@@ -352,10 +375,161 @@ uint32_t tex_features(const hrt_scene* s, uint32_t t, int depth = 0) {
   return 0;
 }
 
+/* ------------------------------------------------------------------ SAH fast path (f4) */
+/* For sphere-only scenes the closest hit does not depend on the BVH (only exact
+ * equal-t ties could), so the device may traverse a better tree than BvhNode::new's median split:
+ * binned SAH, <= LEAF_MAX primitives per leaf, emitted as 8 stackless pre-order streams, one per ray
+ * direction octant, each visiting the near child (by the node's split axis) first. */
+struct SahNode {
+  Aabb box;
+  int axis = 0;
+  int left = -1, right = -1;
+  uint32_t start = 0, count = 0; /* leaf */
+};
+
+struct SahBuilder {
+  std::vector<Aabb> boxes;
+  std::vector<Vec3> cent;
+  std::vector<uint32_t> order;
+  std::vector<SahNode> nodes;
+
+  static float area(const Aabb& b) {
+    Vec3 d = b.mx - b.mn;
+    return 2.0f * (d.x * d.y + d.y * d.z + d.z * d.x);
+  }
+  int build(uint32_t begin, uint32_t end) {
+    SahNode n;
+    Aabb bb = boxes[order[begin]];
+    Vec3 cmn = cent[order[begin]], cmx = cmn;
+    for (uint32_t i = begin; i < end; i++) {
+      bb = surrounding(bb, boxes[order[i]]);
+      Vec3 c = cent[order[i]];
+      for (int a = 0; a < 3; a++) { cmn[a] = std::min(cmn[a], c[a]); cmx[a] = std::max(cmx[a], c[a]); }
+    }
+    n.box = bb;
+    const uint32_t cnt = end - begin;
+    const float C_TRAV = 1.0f, C_ISECT = 2.0f;
+    float best = cnt * C_ISECT;
+    int best_axis = -1, best_bin = -1;
+    const int NB = 16;
+    if (cnt > 1) {
+      for (int a = 0; a < 3; a++) {
+        float ext = cmx[a] - cmn[a];
+        if (!(ext > 0.0f)) continue;
+        Aabb bbox[NB];
+        uint32_t bcnt[NB] = {0};
+        for (uint32_t i = begin; i < end; i++) {
+          int b = std::min(NB - 1, (int)((cent[order[i]][a] - cmn[a]) / ext * NB));
+          bbox[b] = bcnt[b] ? surrounding(bbox[b], boxes[order[i]]) : boxes[order[i]];
+          bcnt[b]++;
+        }
+        Aabb racc[NB];
+        uint32_t rn[NB];
+        Aabb acc;
+        uint32_t accn = 0;
+        for (int b = NB - 1; b >= 1; b--) {
+          if (bcnt[b]) { acc = accn ? surrounding(acc, bbox[b]) : bbox[b]; accn += bcnt[b]; }
+          racc[b] = acc;
+          rn[b] = accn;
+        }
+        Aabb lacc;
+        uint32_t ln = 0;
+        for (int b = 0; b < NB - 1; b++) {
+          if (bcnt[b]) { lacc = ln ? surrounding(lacc, bbox[b]) : bbox[b]; ln += bcnt[b]; }
+          if (ln == 0 || rn[b + 1] == 0) continue;
+          float cost = C_TRAV + C_ISECT * (area(lacc) * ln + area(racc[b + 1]) * rn[b + 1]) / std::max(area(bb), 1e-30f);
+          if (cost < best) { best = cost; best_axis = a; best_bin = b; }
+        }
+      }
+    }
+    if (best_axis < 0 && cnt <= gpu::LEAF_MAX) {
+      n.start = begin;
+      n.count = cnt;
+      nodes.push_back(n);
+      return (int)nodes.size() - 1;
+    }
+    uint32_t mid;
+    if (best_axis >= 0) {
+      float ext = cmx[best_axis] - cmn[best_axis];
+      auto it = std::stable_partition(order.begin() + begin, order.begin() + end, [&](uint32_t p) {
+        int b = std::min(NB - 1, (int)((cent[p][best_axis] - cmn[best_axis]) / ext * NB));
+        return b <= best_bin;
+      });
+      mid = (uint32_t)(it - order.begin());
+      n.axis = best_axis;
+    } else { /* identical centroids: split by count along the widest box axis */
+      Vec3 d = bb.mx - bb.mn;
+      n.axis = (d.x >= d.y && d.x >= d.z) ? 0 : (d.y >= d.z ? 1 : 2);
+      mid = begin + cnt / 2;
+    }
+    if (mid == begin || mid == end) mid = begin + cnt / 2;
+    nodes.push_back(n);
+    int me = (int)nodes.size() - 1;
+    int l = build(begin, mid);
+    int r = build(mid, end);
+    nodes[me].left = l;
+    nodes[me].right = r;
+    return me;
+  }
+};
+
+void emit_stream(hrt_scene* s, const SahBuilder& B, int ni, int octant, uint32_t base) {
+  const SahNode& n = B.nodes[ni];
+  G::Node g;
+  memset(&g, 0, sizeof(g));
+  for (int a = 0; a < 3; a++) { g.mn[a] = n.box.mn[a]; g.mx[a] = n.box.mx[a]; }
+  uint32_t me = (uint32_t)s->f_nodes.size();
+  if (n.left < 0) {
+    g.kp = (G::K_BOX_LEAF << 24) | n.start | ((n.count - 1) << 21);
+    g.skip = me + 1;
+    s->f_nodes.push_back(g);
+    return;
+  }
+  g.kp = G::K_BOX << 24;
+  s->f_nodes.push_back(g);
+  bool neg = (octant >> n.axis) & 1;
+  emit_stream(s, B, neg ? n.right : n.left, octant, base);
+  emit_stream(s, B, neg ? n.left : n.right, octant, base);
+  s->f_nodes[me].skip = (uint32_t)s->f_nodes.size();
+}
+
+void build_fast(hrt_scene* s) {
+  s->f_nodes.clear();
+  s->f_prims.clear();
+  s->f_stream_len = 0;
+  const size_t np = s->g_prims.size();
+  if (np == 0 || np >= (1u << 21)) return;
+  SahBuilder B;
+  for (size_t i = 0; i < np; i++) {
+    const G::Prim& p = s->g_prims[i];
+    Vec3 c0 = v3(p.p0[0], p.p0[1], p.p0[2]);
+    Vec3 rv = v3(p.p0[3], p.p0[3], p.p0[3]);
+    Aabb b{c0 - rv, c0 + rv};
+    if ((p.km & 3u) == G::P_MOVING) { /* box over the BVH build interval [0, 1] (application.rs builders) */
+      Vec3 dc = v3(p.p1[0], p.p1[1], p.p1[2]);
+      Vec3 ca = c0 + ((0.0f - p.p1[3]) / p.p2[0]) * dc, cb = c0 + ((1.0f - p.p1[3]) / p.p2[0]) * dc;
+      b = surrounding(Aabb{ca - rv, ca + rv}, Aabb{cb - rv, cb + rv});
+    }
+    for (int a = 0; a < 3; a++)
+      if (!(b.mn[a] <= b.mx[a])) return; /* NaN / inverted: keep the reference traversal */
+    B.boxes.push_back(b);
+    B.cent.push_back((b.mn + b.mx) * 0.5f);
+    B.order.push_back((uint32_t)i);
+  }
+  int root = B.build(0, (uint32_t)np);
+  for (uint32_t i = 0; i < np; i++) s->f_prims.push_back(s->g_prims[B.order[i]]);
+  for (int o = 0; o < 8; o++) {
+    uint32_t base = (uint32_t)s->f_nodes.size();
+    emit_stream(s, B, root, o, base);
+    if (o == 0) s->f_stream_len = (uint32_t)s->f_nodes.size();
+  }
+}
+
 void flatten(hrt_scene* s) {
   s->g_nodes.clear(); s->g_prims.clear(); s->g_insts.clear(); s->g_media.clear();
   s->g_mats.clear(); s->g_texs.clear();
   s->feature_mask = 0;
+  s->all_boxes_ok = true;
   /* materials and textures first (media append their isotropic materials after these) */
   for (const HMat& m : s->mats) {
     G::Mat g;
@@ -401,8 +575,12 @@ void flatten(hrt_scene* s) {
    * geometry; rect boxes do not (ZX swap, edge-on faces) and instances/media change the ray, so
    * those scenes keep the reference's per-axis test ("culling"). */
   bool sphere_only = (s->feature_mask & (G::F_RECT | G::F_INSTANCE | G::F_MEDIUM)) == 0;
-  s->cull_mode = sphere_only ? G::CULL_SLAB : G::CULL_REFERENCE;
+  s->cull_mode = G::CULL_EXACT;
   s->ln_e = ln_f(E_F);
+  s->f_nodes.clear();
+  s->f_prims.clear();
+  s->f_stream_len = 0;
+  if (sphere_only && (s->feature_mask & ~G::F_BASIC) == 0) build_fast(s); /* opt-in approximate path */
 }
 
 }  // namespace
@@ -773,6 +951,19 @@ hrt_status hrt_scene_get_info(const hrt_scene* s, hrt_scene_info* info) {
     info->in_lds = ((s->feature_mask & ~G::F_BASIC) == 0 &&
                     s->main_end * sizeof(G::Node) + s->g_prims.size() * sizeof(G::Prim) <= 72 * 1024) ? 1u : 0u;
     info->cull_mode = (uint32_t)s->cull_mode;
+    info->sah_stream_len = s->f_stream_len;
+    if (s->f_stream_len) /* the plan the renderer uses for a [0,1] shutter (render.hip plan()) */
+      info->in_lds = 8 * s->f_stream_len * sizeof(G::Node) + s->f_prims.size() * sizeof(G::Prim) <= 150 * 1024 ? 1u : 0u;
+  });
+}
+
+/* Diagnostics: the flattened record of primitive `index` (order 0: reference pre-order, 1: SAH). */
+hrt_status hrt_debug_prim_record(const hrt_scene* s, int32_t order, uint32_t index, float* out12) {
+  return guard([&] {
+    need(s && out12, HRT_ERR_INVALID_ARG, "bad argument");
+    const std::vector<G::Prim>& v = order == 1 ? s->f_prims : s->g_prims;
+    need(index < v.size(), HRT_ERR_INVALID_ARG, "prim index out of range (commit first)");
+    memcpy(out12, &v[index], sizeof(G::Prim));
   });
 }
 

@@ -84,8 +84,17 @@ struct hrt_scene {
   std::vector<hrt::gpu::Mat> g_mats;
   std::vector<hrt::gpu::Tex> g_texs;
   uint32_t main_end = 0;
+  /* SAH fast path (sphere-only scenes, slab culling): 8 pre-order streams of equal length, one per
+   * ray-direction octant (near child first), over a reordered copy of the primitives. */
+  std::vector<hrt::gpu::Node> f_nodes;
+  std::vector<hrt::gpu::Prim> f_prims;
+  uint32_t f_stream_len = 0;
+  size_t off_fnodes = 0, off_fprims = 0;
   uint32_t feature_mask = 0;
   int cull_mode = hrt::gpu::CULL_REFERENCE;
+  bool all_boxes_ok = true;         /* no NODE_REF_ONLY node (slab culling is geometrically safe) */
+  float box_t0 = -3.40282347e+38f;  /* every BVH box is valid for ray times in [box_t0, box_t1] */
+  float box_t1 = 3.40282347e+38f;
   float ln_e = 0; /* ln(E) as computed by hd_math (constant_medium.rs:59) */
 
   /* ---- device ---- */

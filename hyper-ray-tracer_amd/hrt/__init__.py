@@ -102,7 +102,7 @@ class PresetInfo(ctypes.Structure):
 class SceneInfo(ctypes.Structure):
     _fields_ = [
         (n, ctypes.c_uint32)
-        for n in ("nodes", "prims", "materials", "textures", "instances", "media", "feature_mask", "blob_bytes", "in_lds", "cull_mode")
+        for n in ("nodes", "prims", "materials", "textures", "instances", "media", "feature_mask", "blob_bytes", "in_lds", "cull_mode", "sah_stream_len")
     ]
 
 
@@ -115,7 +115,7 @@ EXPORTS = [
     "hrt_node_rotate", "hrt_node_constant_medium", "hrt_node_list", "hrt_node_bvh", "hrt_node_count",
     "hrt_node_bounding_box", "hrt_scene_set_root", "hrt_scene_commit", "hrt_preset_build", "hrt_camera_init",
     "hrt_render_tiles_device", "hrt_render_device", "hrt_render", "hrt_tile_grid", "hrt_scene_get_info",
-    "hrt_debug_device_math",
+    "hrt_debug_device_math", "hrt_debug_trace_path", "hrt_debug_prim_record",
 ]
 
 _lib = None
@@ -177,6 +177,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hrt_tile_grid": (S, [u32, u32, u32, u32, u32, vp, u32, _U32P]),
         "hrt_scene_get_info": (S, [vp, ctypes.POINTER(SceneInfo)]),
         "hrt_debug_device_math": (S, [i32, vp, vp, vp, u32]),
+        "hrt_debug_prim_record": (S, [vp, i32, u32, vp]),
+        "hrt_debug_trace_path": (S, [vp, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), u32, u32, u32, u32, vp, _U32P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -352,6 +354,9 @@ def preset_camera(info: PresetInfo, width: int, height: int) -> Camera:
 
 RENDER_COUNT_WORK = 1
 RENDER_NO_LDS = 2
+RENDER_REFERENCE_CULL = 8
+RENDER_FAST_CULL = 16
+RENDER_SAH = 32
 
 
 def params(width, height, samples, max_depth=50, seed=1, background=(0.7, 0.8, 1.0), t_min=0.001, sample_offset=0, flags=0) -> RenderParams:
@@ -396,4 +401,22 @@ def device_math(op: int, x: np.ndarray, y: Optional[np.ndarray] = None) -> np.nd
     out = np.zeros_like(x)
     yy = None if y is None else np.ascontiguousarray(y, np.float32)
     _check(load().hrt_debug_device_math(op, x.ctypes.data, None if yy is None else yy.ctypes.data, out.ctypes.data, x.size))
+    return out
+
+
+def trace_path(scene: Scene, cam: Camera, p: RenderParams, x: int, y: int, sample: int, max_segments: int = 64):
+    """Device trace of one path: list of (origin, direction, time, t, winner) per segment, radiance."""
+    out = np.zeros(9 * max_segments + 3, np.float32)
+    n = ctypes.c_uint32()
+    _check(load().hrt_debug_trace_path(scene.h, ctypes.byref(cam), ctypes.byref(p), x, y, sample, max_segments, out.ctypes.data, ctypes.byref(n)))
+    segs = []
+    for i in range(min(n.value, max_segments)):
+        r = out[9 * i:9 * i + 9]
+        segs.append((r[0:3].copy(), r[3:6].copy(), float(r[6]), float(r[7]), int(r[8:9].view(np.uint32)[0])))
+    return segs, out[9 * max_segments:9 * max_segments + 3].copy()
+
+
+def prim_record(scene: Scene, index: int, order: int = 0) -> np.ndarray:
+    out = np.zeros(12, np.float32)
+    _check(load().hrt_debug_prim_record(scene.h, order, index, out.ctypes.data))
     return out

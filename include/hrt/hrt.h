@@ -81,7 +81,12 @@ typedef struct hrt_render_params {
 enum {
   HRT_RENDER_COUNT_WORK = 1, /* instrumented kernel: stats also count node visits / prim tests / texture
                                 evaluations (for the algorithmic-bytes model; slower) */
-  HRT_RENDER_NO_LDS = 2      /* keep the scene in global memory even when it fits in LDS (A/B) */
+  HRT_RENDER_NO_LDS = 2,     /* keep the scene in global memory even when it fits in LDS (A/B) */
+  HRT_RENDER_REFERENCE_CULL = 8, /* aabb.rs's per-axis box test alone (the verbatim reference traversal) */
+  HRT_RENDER_FAST_CULL = 16,     /* APPROXIMATE: plain slab culling; differs from the reference on ~1e-7 of
+                                    rays (f32 grazing hits the reference accepts outside a box) */
+  HRT_RENDER_SAH = 32            /* APPROXIMATE, with FAST_CULL on sphere-only scenes: SAH octant streams
+                                    (traversal order changes which of two near-equal f32 hits wins) */
 };
 
 typedef struct hrt_tile {
@@ -219,11 +224,20 @@ typedef struct hrt_scene_info {
   uint32_t feature_mask;
   uint32_t blob_bytes;     /* device bytes of the flattened scene */
   uint32_t in_lds;         /* 1 if the megakernel stages the scene in LDS */
-  uint32_t cull_mode;      /* 0: reference per-axis box test (aabb.rs), 1: slab test */
+  uint32_t cull_mode;      /* default culling: 2 = exact (reference test + provably safe extra culling) */
+  uint32_t sah_stream_len; /* >0: sphere-only scene with the SAH octant streams (8 x this many nodes) */
 } hrt_scene_info;
 hrt_status hrt_scene_get_info(const hrt_scene* s, hrt_scene_info* info);
 /* Evaluate the shared deterministic math on the DEVICE (op: 0 sin,1 cos,2 acos,3 atan2,4 ln,
  * 5 pow5, 6 tan) for n inputs; used by the GPU KAT test to prove host/device bit identity. */
+/* Trace ONE path (pixel x,y of the full image; sample index) on the device with the traversal the
+ * renderer would use for these params; out[9*i .. 9*i+8] = origin, direction, time, closest t,
+ * winner id (bits) of segment i; out[9*max_segments .. +2] = the path's radiance. */
+hrt_status hrt_debug_trace_path(hrt_scene* s, const hrt_camera* cam, const hrt_render_params* p, uint32_t x,
+                                uint32_t y, uint32_t sample, uint32_t max_segments, float* out,
+                                uint32_t* n_segments);
+/* The flattened 48-byte record of a primitive (order 0: reference pre-order, 1: SAH streams). */
+hrt_status hrt_debug_prim_record(const hrt_scene* s, int32_t order, uint32_t index, float* out12);
 hrt_status hrt_debug_device_math(int32_t op, const float* x, const float* y, float* out, uint32_t n);
 
 #ifdef __cplusplus
