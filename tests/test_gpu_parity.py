@@ -145,3 +145,46 @@ def test_multi_tile_call_matches_full_frame(earth):
             covered[y:y + h, x:x + w] = True
             off += w * h
     assert covered.all()
+
+
+# The verbatim reference traversal (HRT_RENDER_REFERENCE_CULL: aabb.rs's per-axis test alone) is
+# checked against the oracle above; the default EXACT culling must give the same bits as it at sizes
+# the oracle cannot reach.
+EXACT_CASES = [
+    ("random", 320, 180, 16), ("two_spheres", 320, 180, 16), ("two_perlin_spheres", 320, 180, 16),
+    ("earth", 320, 180, 16), ("simple_light", 320, 180, 16), ("cornell", 256, 256, 16),
+    ("cornell_smoke", 256, 256, 16), ("final", 200, 200, 8), ("earth_perlin", 320, 180, 16),
+    ("random_10k", 320, 180, 8), ("features", 320, 180, 16),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,w,h,spp", EXACT_CASES)
+def test_exact_culling_bit_identical_to_reference_traversal(name, w, h, spp, earth):
+    s = hrt.preset(name, 1, earth)
+    s.commit()
+    cam = hrt.preset_camera(s.info, w, h)
+    bg = tuple(s.info.background)
+    ref, st_ref = hrt.render(s, cam, hrt.params(w, h, spp, 50, 13, bg, flags=hrt.RENDER_REFERENCE_CULL), stats=True)
+    ex, st_ex = hrt.render(s, cam, hrt.params(w, h, spp, 50, 13, bg), stats=True)
+    assert st_ex.segments == st_ref.segments
+    assert np.array_equal(ex, ref)
+
+
+@pytest.mark.gpu
+def test_headline_frame_exact_equals_reference_traversal(earth):
+    """BASELINE config 2 at full size: 1920x1080, 500 spp, depth 50 (2.9 G rays): the default path is
+    bit-identical to the verbatim reference traversal; properties: finite, alpha 1, deterministic."""
+    s = hrt.preset("random", 1, earth)
+    s.commit()
+    W, H = 1920, 1080
+    cam = hrt.preset_camera(s.info, W, H)
+    bg = tuple(s.info.background)
+    ex, st = hrt.render(s, cam, hrt.params(W, H, 500, 50, 1, bg), stats=True)
+    ref, st_ref = hrt.render(s, cam, hrt.params(W, H, 500, 50, 1, bg, flags=hrt.RENDER_REFERENCE_CULL), stats=True)
+    assert st.samples == W * H * 500 and st.pixels == W * H
+    assert st.segments == st_ref.segments
+    assert np.array_equal(ex, ref)
+    assert np.isfinite(ex).all() and (ex[..., 3] == 1).all()
+    again = hrt.render(s, cam, hrt.params(W, H, 500, 50, 1, bg))
+    assert np.array_equal(again, ex)
