@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -69,100 +70,127 @@ struct KParams {
   uint32_t n_prims;
   uint32_t n_nodes;    /* node-stream entries to stage in LDS */
   uint32_t stream_len; /* FAST: length of one octant stream */
+  uint32_t postpone;   /* BASIC kernel: lanes that must have finished their walk before a wave shades */
+  uint32_t motion_uniform; /* every moving sphere has time0 = motion_t0, time1 - time0 = motion_span */
+  float motion_t0, motion_span;
   float4* partial; /* [n_chunks][n_out] chunk sums (n_chunks > 1) */
 };
 
 /* per-lane work counters of the instrumented (COUNT) instantiation */
 struct Counts {
   uint32_t nodes, prims, tex;
+  uint32_t walk_slots, shade_slots; /* lane slots of wave iterations: walk (node) loop, shading passes */
+  uint32_t prim_slots;              /* lane slots of wave executions of the primitive block */
 };
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+  return v;
+}
 
 struct TRay {
   Vec3 o, d, inv;
   float time;
-  float dd; /* dot(d, d): sphere.rs:42 `a`, constant for the ray */
+  float dd;  /* dot(d, d): sphere.rs:42 `a`, constant for the ray */
+  float rdd; /* RN(1 / dd), for div_dd */
+  float tau; /* (time - time0) / (time1 - time0) of the scene's moving spheres (uniform motion only) */
 };
 
-__device__ __forceinline__ void set_ray(TRay& r, Vec3 o, Vec3 d, float time) {
+/* x / r.dd correctly rounded (bit-identical to IEEE division) in 3 instructions instead of the
+ * ~11 of the general sequence: with y = RN(1/a), q0 = RN(x*y) is within one ulp of x/a, the
+ * residual x - q0*a is exact in an fma, and RN(q0 + residual*y) is RN(x/a) (Markstein's theorem;
+ * no under/overflow anywhere while |x|, |q0|, a lie in [2^-100, 2^100]).  Zero, NaN, inf and
+ * extreme exponents take the IEEE sequence.  tests/test_fast_division.py checks 6e7 cases on the host
+ * and 4e6 on the device (3e9 more were checked while writing it). */
+__device__ __forceinline__ float div_rn(float x, float a, float y) {
+  const float q0 = x * y;
+  const float q = fmaf(fmaf(-q0, a, x), y, q0);
+  const float ax = fabsf(x), aq = fabsf(q0);
+  const bool fast = ax >= 0x1p-100f && ax <= 0x1p100f && aq >= 0x1p-100f && aq <= 0x1p100f &&
+                    a >= 0x1p-100f && a <= 0x1p100f;
+  return fast ? q : x / a;
+}
+
+/* a new origin/direction; the ray keeps its time */
+__device__ __forceinline__ void set_dir(TRay& r, Vec3 o, Vec3 d) {
   r.o = o;
   r.d = d;
-  r.time = time;
   /* aabb.rs:22 computes 1/d per call; the value is the same every time */
   r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
   r.dd = dot(d, d);
+  r.rdd = 1.0f / r.dd;
+}
+
+__device__ __forceinline__ void set_time(TRay& r, float time, const KParams& P) {
+  r.time = time;
+  /* moving_sphere.rs:55-58: identical for every moving sphere when they share time0/time1 */
+  r.tau = P.motion_uniform ? (time - P.motion_t0) / P.motion_span : 0.0f;
+}
+
+__device__ __forceinline__ void set_ray(TRay& r, Vec3 o, Vec3 d, float time, const KParams& P) {
+  set_dir(r, o, d);
+  set_time(r, time, P);
 }
 
 __device__ __forceinline__ float4 ld4(const void* p) { return *reinterpret_cast<const float4*>(p); }
 
 /* aabb.rs:20-47 (CULL_REFERENCE), its narrowed form (CULL_SLAB), or CULL_EXACT: the reference test
- * AND an inflated slab test that only rejects boxes no accepted hit can come from (layout.h). */
+ * AND an inflated slab test that only rejects boxes no accepted hit can come from (layout.h).
+ * `if t0 > t_min {t0} else {t_min}` (aabb.rs:30-35) is fmaxf(t0, t_min): in IEEE mode v_max_f32
+ * returns the non-NaN operand exactly as the comparison form does (a NaN t0 leaves t_min), and the
+ * forms differ at most in the sign of a zero, which the `t_max <= t_min` test (:36) cannot see. */
 template <int CULL>
 __device__ __forceinline__ bool box_hit(const float4& a, const float4& b, const TRay& r, float tmin,
                                         float tmax, bool ref_only = false) {
   const float mn[3] = {a.x, a.y, a.z}, mx[3] = {b.x, b.y, b.z};
   const float o[3] = {r.o.x, r.o.y, r.o.z}, inv[3] = {r.inv.x, r.inv.y, r.inv.z};
-  if (CULL == G::CULL_EXACT) {
-    float dmn[3], dmx[3];
-    float dist = 0.0f;
+  float dmn[3], dmx[3];
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-      dmn[k] = mn[k] - o[k];
-      dmx[k] = mx[k] - o[k];
-      dist = fmaxf(dist, fmaxf(fabsf(dmn[k]), fabsf(dmx[k])));
-    }
-    const float margin = G::EXACT_MARGIN * dist;
-    bool ok = true;
-    float lo = tmin, hi = tmax;
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      float ts = dmn[k] * inv[k];
-      float te = dmx[k] * inv[k];
-      if (inv[k] < 0.0f) { float t = ts; ts = te; te = t; }
-      float l1 = ts > tmin ? ts : tmin;
-      float h1 = te < tmax ? te : tmax;
-      ok = ok & !(h1 <= l1);
-      const float w = margin * fabsf(inv[k]);
-      const float ts2 = ts - w, te2 = te + w;
-      lo = ts2 > lo ? ts2 : lo;
-      hi = te2 < hi ? te2 : hi;
-    }
-    return ok & (ref_only | !(hi < lo));
+  for (int k = 0; k < 3; k++) {
+    dmn[k] = mn[k] - o[k];
+    dmx[k] = mx[k] - o[k];
   }
-  if (CULL == G::CULL_REFERENCE) {
-    bool ok = true;
+  float ts[3], te[3];
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-      float ts = (mn[k] - o[k]) * inv[k];
-      float te = (mx[k] - o[k]) * inv[k];
-      if (inv[k] < 0.0f) { float t = ts; ts = te; te = t; }
-      float lo = ts > tmin ? ts : tmin;
-      float hi = te < tmax ? te : tmax;
-      ok = ok & !(hi <= lo);
-    }
-    return ok;
-  } else {
-    float lo = tmin, hi = tmax;
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      float ts = (mn[k] - o[k]) * inv[k];
-      float te = (mx[k] - o[k]) * inv[k];
-      if (inv[k] < 0.0f) { float t = ts; ts = te; te = t; }
-      lo = ts > lo ? ts : lo;
-      hi = te < hi ? te : hi;
-    }
+  for (int k = 0; k < 3; k++) {
+    const float t0 = dmn[k] * inv[k], t1 = dmx[k] * inv[k];
+    const bool neg = inv[k] < 0.0f; /* aabb.rs:28-29 swap */
+    ts[k] = neg ? t1 : t0;
+    te[k] = neg ? t0 : t1;
+  }
+  if (CULL == G::CULL_SLAB) {
+    const float lo = fmaxf(fmaxf(fmaxf(ts[0], tmin), ts[1]), ts[2]);
+    const float hi = fminf(fminf(fminf(te[0], tmax), te[1]), te[2]);
     return !(hi <= lo);
   }
+  bool ok = true; /* the reference: each axis on its own against [t_min, t_max] */
+#pragma unroll
+  for (int k = 0; k < 3; k++) ok = ok & !(fminf(te[k], tmax) <= fmaxf(ts[k], tmin));
+  if (CULL == G::CULL_REFERENCE) return ok;
+  /* CULL_EXACT: the slab interval widened by margin(box) / |d_k| per axis */
+  float dist = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 3; k++) dist = fmaxf(dist, fmaxf(fabsf(dmn[k]), fabsf(dmx[k])));
+  const float margin = G::EXACT_MARGIN * dist;
+  float lo = tmin, hi = tmax;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const float w = margin * fabsf(inv[k]);
+    lo = fmaxf(lo, ts[k] - w);
+    hi = fminf(hi, te[k] + w);
+  }
+  return ok & (ref_only | !(hi < lo));
 }
 
 /* sphere.rs:38-55 / moving_sphere.rs:61-78: the accepted root only */
 __device__ __forceinline__ bool sphere_root(const G::Prim* pp, uint32_t kind, const TRay& r, float tmin,
-                                            float tmax, float& root) {
+                                            float tmax, float& root, bool motion_uniform) {
   float4 p0 = ld4(pp->p0);
   Vec3 c = v3(p0.x, p0.y, p0.z);
   if (kind == G::P_MOVING) {
     float4 p1 = ld4(pp->p1);
-    float span = pp->p2[0];
-    c = c + ((r.time - p1.w) / span) * v3(p1.x, p1.y, p1.z);
+    const float f = motion_uniform ? r.tau : (r.time - p1.w) / pp->p2[0];
+    c = c + f * v3(p1.x, p1.y, p1.z);
   }
   Vec3 oc = r.o - c;
   float a = r.dd;
@@ -171,9 +199,9 @@ __device__ __forceinline__ bool sphere_root(const G::Prim* pp, uint32_t kind, co
   float disc = half_b * half_b - a * cc;
   if (disc < 0.0f) return false;
   float sq = sqrtf(disc);
-  float t = (-half_b - sq) / a;
+  float t = div_rn(-half_b - sq, a, r.rdd);
   if (t < tmin || tmax < t) {
-    t = (-half_b + sq) / a;
+    t = div_rn(-half_b + sq, a, r.rdd);
     if (t < tmin || tmax < t) return false;
   }
   root = t;
@@ -233,7 +261,7 @@ __device__ void trace(const KParams& P, const G::Node* __restrict__ nodes, const
                       uint32_t begin, uint32_t end, Vec3 o, Vec3 d, float time, float tmin, float& closest,
                       uint32_t& winner, const PathKey& pk, Counts& cn) {
   TRay r;
-  set_ray(r, o, d, time);
+  set_ray(r, o, d, time, P);
   if constexpr (FAST) { /* the stream whose near-child order matches the ray's direction octant */
     const uint32_t oct = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
     begin = oct * P.stream_len;
@@ -266,7 +294,7 @@ __device__ void trace(const KParams& P, const G::Node* __restrict__ nodes, const
         const G::Prim* pp = prims + start + k;
         if constexpr (COUNT) cn.prims++;
         float t;
-        if (sphere_root(pp, pp->km & 3u, r, tmin, closest, t)) {
+        if (sphere_root(pp, pp->km & 3u, r, tmin, closest, t, P.motion_uniform != 0)) {
           closest = t;
           winner = start + k;
         }
@@ -292,10 +320,10 @@ __device__ void trace(const KParams& P, const G::Node* __restrict__ nodes, const
           sp++;
           Vec3 no = r.o, nd = r.d;
           inst_ray(P.insts[payload], no, nd);
-          set_ray(r, no, nd, r.time);
+          set_dir(r, no, nd);
         } else if (kind == G::K_INST_END) {
           sp--;
-          set_ray(r, so[sp], sd[sp], r.time);
+          set_dir(r, so[sp], sd[sp]);
         } else if (kind == G::K_MEDIUM) {
           if constexpr (MEDIA) {
             /* constant_medium.rs:34-76 */
@@ -332,7 +360,7 @@ __device__ void trace(const KParams& P, const G::Node* __restrict__ nodes, const
     float t;
     bool h;
     if (FULL && pkind == G::P_RECT) h = rect_t(pp, (km >> 2) & 3u, r, tmin, closest, t);
-    else h = sphere_root(pp, pkind, r, tmin, closest, t);
+    else h = sphere_root(pp, pkind, r, tmin, closest, t, P.motion_uniform != 0);
     if (h) {
       closest = t;
       winner = FULL ? here : payload; /* BASIC kernels name the primitive directly */
@@ -364,7 +392,7 @@ __device__ __forceinline__ void sphere_uv(Vec3 p, float& u, float& v) {
 /* Record of the winning leaf in world space (hit_record.rs, sphere.rs:57-73, rect.rs:70-83,
  * constant_medium.rs:66-75, then translation.rs:33-35 / rotation.rs:119-132 on the way out). */
 template <bool FULL>
-__device__ Rec make_record(const KParams& P, uint32_t winner, float t, Vec3 wo, Vec3 wd, float time) {
+__device__ Rec make_record(const KParams& P, uint32_t winner, float t, Vec3 wo, Vec3 wd, float time, float tau) {
   Rec rec;
   rec.u = 0.0f;
   rec.v = 0.0f;
@@ -375,7 +403,8 @@ __device__ Rec make_record(const KParams& P, uint32_t winner, float t, Vec3 wo, 
     Vec3 c = v3(p0.x, p0.y, p0.z);
     if ((km & 3u) == G::P_MOVING) {
       float4 p1 = ld4(pp->p1);
-      c = c + ((time - p1.w) / pp->p2[0]) * v3(p1.x, p1.y, p1.z);
+      const float f = P.motion_uniform ? tau : (time - p1.w) / pp->p2[0];
+      c = c + f * v3(p1.x, p1.y, p1.z);
     }
     rec.mat = km >> 4;
     Vec3 at = wo + t * wd;
@@ -426,7 +455,8 @@ __device__ Rec make_record(const KParams& P, uint32_t winner, float t, Vec3 wo, 
         Vec3 c = v3(p0.x, p0.y, p0.z);
         if (pkind == G::P_MOVING) {
           float4 p1 = ld4(pp->p1);
-          c = c + ((time - p1.w) / pp->p2[0]) * v3(p1.x, p1.y, p1.z);
+          const float f = P.motion_uniform ? tau : (time - p1.w) / pp->p2[0];
+          c = c + f * v3(p1.x, p1.y, p1.z);
         }
         Vec3 at = o + t * d;
         Vec3 outward = (at - c) / p0.w;
@@ -557,29 +587,17 @@ __device__ __forceinline__ void start_sample(const KParams& P, PathState& ps, ui
   ps.depth_left = P.max_depth;
 }
 
-/* One step of ray_color (application.rs:477-495).  Returns true when the path is finished.
- * dbg (debug kernel only): receives o, d, time, t, winner of the traced segment. */
-template <int CULL, bool FULL, bool COUNT, bool FAST>
-__device__ __forceinline__ bool segment(const KParams& P, const G::Node* nodes, const G::Prim* prims,
-                                        PathState& ps, Counts& cn, float* dbg) {
-  ps.traced = false;
-  if (ps.depth_left == 0) return true; /* depth cap: black (:478-480) */
-  float closest = __uint_as_float(0x7f800000u);
-  uint32_t winner = G::NONE;
-  trace<CULL, FULL, FULL, COUNT, FAST>(P, nodes, prims, 0u, P.main_end, ps.ro, ps.rd, ps.rtime, P.t_min, closest,
-                                       winner, ps.pk, cn);
-  ps.traced = true;
-  ps.pk.segment++;
-  if (dbg) {
-    dbg[0] = ps.ro.x; dbg[1] = ps.ro.y; dbg[2] = ps.ro.z;
-    dbg[3] = ps.rd.x; dbg[4] = ps.rd.y; dbg[5] = ps.rd.z;
-    dbg[6] = ps.rtime; dbg[7] = closest; dbg[8] = __uint_as_float(winner);
-  }
+/* The part of one ray_color step after world.hit (application.rs:483-494): background on a miss,
+ * else hit record, emission and scatter.  (ro, rd, rtime) is the segment just traced; the scattered
+ * ray goes to ps.ro/ps.rd.  Returns true when the path is finished. */
+template <bool FULL, bool COUNT>
+__device__ __forceinline__ bool shade(const KParams& P, PathState& ps, uint32_t winner, float closest, Vec3 ro,
+                                      Vec3 rd, float rtime, float tau, Counts& cn) {
   if (winner == G::NONE) {
     ps.rad = ps.rad + mul_elem(ps.thr, P.background);
     return true;
   }
-  Rec rec = make_record<FULL>(P, winner, closest, ps.ro, ps.rd, ps.rtime);
+  Rec rec = make_record<FULL>(P, winner, closest, ro, rd, rtime, tau);
   const G::Mat M = P.mats[rec.mat];
   Vec3 emitted = v3(0.0f, 0.0f, 0.0f);
   Vec3 att = v3(0.0f, 0.0f, 0.0f), ndir = v3(0.0f, 0.0f, 0.0f);
@@ -591,13 +609,13 @@ __device__ __forceinline__ bool segment(const KParams& P, const G::Node* nodes, 
     att = tex_value<FULL, COUNT>(P, M.tex, rec.u, rec.v, rec.p, cn);
     scattered = true;
   } else if (M.kind == G::M_METAL) { /* metal.rs:29-42 */
-    Vec3 reflected = reflect(normalize(ps.rd), rec.n);
+    Vec3 reflected = reflect(normalize(rd), rec.n);
     ndir = reflected + M.a[3] * random_in_unit_sphere(rng);
     scattered = dot(ndir, rec.n) > 0.0f;
     att = v3(M.a[0], M.a[1], M.a[2]);
   } else if (M.kind == G::M_DIELECTRIC) { /* dielectric.rs:31-55 */
     float ratio = rec.front ? (1.0f / M.a[0]) : M.a[0];
-    Vec3 ud = normalize(ps.rd);
+    Vec3 ud = normalize(rd);
     float cos_theta = min_rs(dot(-ud, rec.n), 1.0f);
     float sin_theta = sqrtf(1.0f - cos_theta * cos_theta);
     bool cannot_refract = (ratio * sin_theta) > 1.0f;
@@ -622,13 +640,35 @@ __device__ __forceinline__ bool segment(const KParams& P, const G::Node* nodes, 
   return false;
 }
 
+/* One step of ray_color (application.rs:477-495).  Returns true when the path is finished.
+ * dbg (debug kernel only): receives o, d, time, t, winner of the traced segment. */
+template <int CULL, bool FULL, bool COUNT, bool FAST>
+__device__ __forceinline__ bool segment(const KParams& P, const G::Node* nodes, const G::Prim* prims,
+                                        PathState& ps, Counts& cn, float* dbg) {
+  ps.traced = false;
+  if (ps.depth_left == 0) return true; /* depth cap: black (:478-480) */
+  float closest = __uint_as_float(0x7f800000u);
+  uint32_t winner = G::NONE;
+  trace<CULL, FULL, FULL, COUNT, FAST>(P, nodes, prims, 0u, P.main_end, ps.ro, ps.rd, ps.rtime, P.t_min, closest,
+                                       winner, ps.pk, cn);
+  ps.traced = true;
+  ps.pk.segment++;
+  if (dbg) {
+    dbg[0] = ps.ro.x; dbg[1] = ps.ro.y; dbg[2] = ps.ro.z;
+    dbg[3] = ps.rd.x; dbg[4] = ps.rd.y; dbg[5] = ps.rd.z;
+    dbg[6] = ps.rtime; dbg[7] = closest; dbg[8] = __uint_as_float(winner);
+  }
+  const float tau = P.motion_uniform ? (ps.rtime - P.motion_t0) / P.motion_span : 0.0f;
+  return shade<FULL, COUNT>(P, ps, winner, closest, ps.ro, ps.rd, ps.rtime, tau, cn);
+}
+
 /* Diagnostics: trace ONE path (pixel, sample) and record every segment (9 floats each). */
 template <int CULL, bool FULL, bool FAST>
 __global__ void debug_path_kernel(KParams P, uint32_t px, uint32_t py, uint32_t sample, float* out,
                                   uint32_t max_seg, uint32_t* n_out) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   PathState ps;
-  Counts cn{0u, 0u, 0u};
+  Counts cn{0u, 0u, 0u, 0u, 0u, 0u};
   start_sample(P, ps, px, py, sample);
   uint32_t n = 0;
   float scratch[9];
@@ -649,29 +689,85 @@ __global__ void debug_path_kernel(KParams P, uint32_t px, uint32_t py, uint32_t 
 template <bool LDS, bool FAST>
 constexpr int block_threads() { return LDS ? (FAST ? 1024 : 512) : 256; }
 
-template <int CULL, bool FULL, bool COUNT, bool LDS, bool FAST>
-__global__ __launch_bounds__((block_threads<LDS, FAST>())) void render_kernel(KParams P) {
-  extern __shared__ float4 lds_scene[];
-  const G::Node* nodes = P.nodes;
-  const G::Prim* prims = P.prims;
-  if constexpr (LDS) {
-    const uint32_t n4 = P.n_nodes * (uint32_t)(sizeof(G::Node) / 16);
-    const uint32_t p4 = P.n_prims * (uint32_t)(sizeof(G::Prim) / 16);
-    const float4* gn = reinterpret_cast<const float4*>(P.nodes);
-    const float4* gp = reinterpret_cast<const float4*>(P.prims);
-    for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) lds_scene[k] = gn[k];
-    for (uint32_t k = threadIdx.x; k < p4; k += blockDim.x) lds_scene[n4 + k] = gp[k];
-    __syncthreads();
-    nodes = reinterpret_cast<const G::Node*>(lds_scene);
-    prims = reinterpret_cast<const G::Prim*>(lds_scene + n4);
-  }
-  const uint32_t lane = threadIdx.x & 63u;
-  const float scale = 1.0f / (float)P.spp; /* application.rs:403 */
+/* Copy the node stream and primitive records into this workgroup's LDS. */
+__device__ __forceinline__ void stage_scene(const KParams& P, float4* lds, const G::Node*& nodes, const G::Prim*& prims) {
+  const uint32_t n4 = P.n_nodes * (uint32_t)(sizeof(G::Node) / 16);
+  const uint32_t p4 = P.n_prims * (uint32_t)(sizeof(G::Prim) / 16);
+  const float4* gn = reinterpret_cast<const float4*>(P.nodes);
+  const float4* gp = reinterpret_cast<const float4*>(P.prims);
+  for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) lds[k] = gn[k];
+  for (uint32_t k = threadIdx.x; k < p4; k += blockDim.x) lds[n4 + k] = gp[k];
+  __syncthreads();
+  nodes = reinterpret_cast<const G::Node*>(lds);
+  prims = reinterpret_cast<const G::Prim*>(lds + n4);
+}
 
-  bool has_item = false, exhausted = false, in_path = false;
-  uint32_t px = 0, py = 0, out_idx = 0, chunk = 0, sample = 0, sample_end = 0;
-  Vec3 sum = v3(0.0f, 0.0f, 0.0f);
-  PathState ps;
+/* A lane's current work item: one pixel and a chunk [sample, sample_end) of its samples. */
+struct Item {
+  uint32_t pxy; /* px | py << 16 */
+  uint32_t out_idx, chunk, sample, sample_end;
+};
+
+/* Idle lanes of the wave claim work items with ONE atomicAdd (ballot + popcount).  Items are
+ * ordered [tile][8x8 block][chunk][64 pixels], so a wave starts on 64 neighbouring pixels. */
+__device__ __forceinline__ void claim_work(const KParams& P, uint32_t lane, bool& has_item, bool& exhausted,
+                                           Item& it) {
+  const bool want = !has_item && !exhausted;
+  const unsigned long long want_mask = __ballot(want);
+  if (!want_mask) return;
+  const uint32_t cnt = (uint32_t)__popcll(want_mask);
+  const int leader = __ffsll((long long)want_mask) - 1;
+  uint32_t base = 0;
+  if ((int)lane == leader) base = atomicAdd(P.counter, cnt);
+  base = __shfl(base, leader);
+  if (!want) return;
+  const uint32_t rank = (uint32_t)__popcll(want_mask & ((1ull << lane) - 1ull));
+  const uint32_t w = base + rank;
+  if (w >= P.total_work) {
+    exhausted = true;
+    return;
+  }
+  /* tile (binary search on pad_start), then [8x8 block][chunk][64 pixels] inside it */
+  uint32_t lo = 0, hi = P.n_tiles - 1;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi + 1) >> 1;
+    if (P.tiles[mid].pad_start <= w) lo = mid; else hi = mid - 1;
+  }
+  const G::TileDev T = P.tiles[lo];
+  const uint32_t q = w - T.pad_start;
+  const uint32_t blk = q / (64u * P.n_chunks), rem = q - blk * 64u * P.n_chunks;
+  const uint32_t c = rem >> 6, in = rem & 63u;
+  const uint32_t lx = (blk % T.bw) * 8u + (in & 7u), ly = (blk / T.bw) * 8u + (in >> 3);
+  if (lx < T.w && ly < T.h) {
+    has_item = true;
+    it.pxy = (T.x + lx) | ((T.y + ly) << 16);
+    it.out_idx = T.out_off + ly * T.w + lx;
+    it.chunk = c;
+    it.sample = c * P.chunk;
+    it.sample_end = min(P.spp, it.sample + P.chunk);
+  }
+}
+
+/* A finished sample: add it to the chunk sum in order (application.rs:448); a finished chunk goes to
+ * the output (one chunk: sqrt(sum/spp), alpha 1, :451-456) or to its partial-sum slot. */
+__device__ __forceinline__ void finish_sample(const KParams& P, Item& it, Vec3& sum, Vec3 rad, float scale,
+                                              bool& has_item, uint32_t& n_samples, uint32_t& n_pixels) {
+  sum = sum + rad;
+  n_samples++;
+  if (++it.sample == it.sample_end) {
+    if (P.n_chunks == 1) {
+      P.out[it.out_idx] = make_float4(sqrtf(sum.x * scale), sqrtf(sum.y * scale), sqrtf(sum.z * scale), 1.0f);
+      n_pixels++;
+    } else {
+      P.partial[(size_t)it.chunk * P.n_out + it.out_idx] = make_float4(sum.x, sum.y, sum.z, 0.0f);
+      if (it.chunk == 0) n_pixels++;
+    }
+    has_item = false;
+    sum = v3(0.0f, 0.0f, 0.0f);
+  }
+}
+
+__device__ __forceinline__ void init_path_state(PathState& ps) {
   ps.rng.s0 = ps.rng.s1 = ps.rng.s2 = ps.rng.s3 = 1u;
   ps.pk = PathKey{0ull, 0u};
   ps.depth_left = 0;
@@ -681,83 +777,217 @@ __global__ __launch_bounds__((block_threads<LDS, FAST>())) void render_kernel(KP
   ps.thr = v3(1.0f, 1.0f, 1.0f);
   ps.rad = v3(0.0f, 0.0f, 0.0f);
   ps.traced = false;
-  uint32_t n_seg = 0, n_samples = 0, n_pixels = 0;
-  Counts cn{0u, 0u, 0u};
+}
 
-  for (;;) {
-    /* ---- claim work items for idle lanes: one atomic per wave ---- */
-    const bool want = !has_item && !exhausted;
-    const unsigned long long want_mask = __ballot(want);
-    if (want_mask) {
-      const uint32_t cnt = (uint32_t)__popcll(want_mask);
-      const int leader = __ffsll((long long)want_mask) - 1;
-      uint32_t base = 0;
-      if ((int)lane == leader) base = atomicAdd(P.counter, cnt);
-      base = __shfl(base, leader);
-      if (want) {
-        const uint32_t rank = (uint32_t)__popcll(want_mask & ((1ull << lane) - 1ull));
-        const uint32_t w = base + rank;
-        if (w >= P.total_work) {
-          exhausted = true;
-        } else {
-          /* tile (binary search on pad_start), then [8x8 block][chunk][64 pixels] inside it */
-          uint32_t lo = 0, hi = P.n_tiles - 1;
-          while (lo < hi) {
-            uint32_t mid = (lo + hi + 1) >> 1;
-            if (P.tiles[mid].pad_start <= w) lo = mid; else hi = mid - 1;
-          }
-          const G::TileDev T = P.tiles[lo];
-          const uint32_t q = w - T.pad_start;
-          const uint32_t blk = q / (64u * P.n_chunks), rem = q - blk * 64u * P.n_chunks;
-          const uint32_t c = rem >> 6, in = rem & 63u;
-          const uint32_t lx = (blk % T.bw) * 8u + (in & 7u), ly = (blk / T.bw) * 8u + (in >> 3);
-          if (lx < T.w && ly < T.h) {
-            has_item = true;
-            px = T.x + lx;
-            py = T.y + ly;
-            out_idx = T.out_off + ly * T.w + lx;
-            chunk = c;
-            sample = c * P.chunk;
-            sample_end = min(P.spp, sample + P.chunk);
-            sum = v3(0.0f, 0.0f, 0.0f);
-            in_path = false;
-          }
-        }
-      }
-    }
-    if (!__any(has_item || !exhausted)) break;
-    if (!has_item) continue;
+__device__ __forceinline__ void flush_counts(const KParams& P, const Counts& cn) {
+  atomicAdd(&P.stats[3], (unsigned long long)cn.nodes);
+  atomicAdd(&P.stats[4], (unsigned long long)cn.prims);
+  atomicAdd(&P.stats[5], (unsigned long long)cn.tex);
+  atomicAdd(&P.stats[6], (unsigned long long)cn.walk_slots);
+  atomicAdd(&P.stats[7], (unsigned long long)cn.shade_slots);
+  atomicAdd(&P.stats[8], (unsigned long long)cn.prim_slots);
+}
 
-    if (!in_path) {
-      start_sample(P, ps, px, py, sample);
-      in_path = true;
-    }
-    const bool done = segment<CULL, FULL, COUNT, FAST>(P, nodes, prims, ps, cn, nullptr);
-    if (ps.traced) n_seg++;
-    if (done) {
-      sum = sum + ps.rad; /* application.rs:448, samples of a chunk in order */
-      in_path = false;
-      n_samples++;
-      if (++sample == sample_end) {
-        if (P.n_chunks == 1) {
-          P.out[out_idx] = make_float4(sqrtf(sum.x * scale), sqrtf(sum.y * scale), sqrtf(sum.z * scale), 1.0f);
-          n_pixels++;
-        } else {
-          P.partial[(size_t)chunk * P.n_out + out_idx] = make_float4(sum.x, sum.y, sum.z, 0.0f);
-          if (chunk == 0) n_pixels++;
-        }
-        has_item = false;
-      }
-    }
-  }
+__device__ __forceinline__ void flush_stats(const KParams& P, uint32_t n_seg, uint32_t n_samples, uint32_t n_pixels,
+                                            const Counts& cn, bool count) {
   atomicAdd(&P.stats[0], (unsigned long long)n_seg);
   atomicAdd(&P.stats[1], (unsigned long long)n_samples);
   atomicAdd(&P.stats[2], (unsigned long long)n_pixels);
-  if constexpr (COUNT) {
+  if (count) {
     atomicAdd(&P.stats[3], (unsigned long long)cn.nodes);
     atomicAdd(&P.stats[4], (unsigned long long)cn.prims);
     atomicAdd(&P.stats[5], (unsigned long long)cn.tex);
+    atomicAdd(&P.stats[6], (unsigned long long)cn.walk_slots);
+    atomicAdd(&P.stats[7], (unsigned long long)cn.shade_slots);
+    atomicAdd(&P.stats[8], (unsigned long long)cn.prim_slots);
   }
+}
+
+/* The general kernel (every feature): each iteration of the wave loop advances every busy lane by
+ * exactly one ray segment.  Lanes whose path ended start their next sample in the same iteration. */
+template <int CULL, bool FULL, bool COUNT, bool LDS, bool FAST>
+__global__ __launch_bounds__((block_threads<LDS, FAST>())) void render_kernel(KParams P) {
+  extern __shared__ float4 lds_scene[];
+  const G::Node* nodes = P.nodes;
+  const G::Prim* prims = P.prims;
+  if constexpr (LDS) stage_scene(P, lds_scene, nodes, prims);
+  const uint32_t lane = threadIdx.x & 63u;
+  const float scale = 1.0f / (float)P.spp; /* application.rs:403 */
+
+  bool has_item = false, exhausted = false, in_path = false;
+  Item it{0u, 0u, 0u, 0u, 0u};
+  Vec3 sum = v3(0.0f, 0.0f, 0.0f);
+  PathState ps;
+  init_path_state(ps);
+  uint32_t n_seg = 0, n_samples = 0, n_pixels = 0;
+  Counts cn{0u, 0u, 0u, 0u, 0u, 0u};
+
+  uint32_t seg_nodes = 0; /* COUNT: node visits of this lane's last segment */
+  for (;;) {
+    if constexpr (COUNT) { /* every lane is active here: the walk took as long as its longest lane */
+      cn.walk_slots += wave_max(seg_nodes);
+      cn.shade_slots++;
+      seg_nodes = 0;
+    }
+    claim_work(P, lane, has_item, exhausted, it);
+    if (!__any(has_item || !exhausted)) break;
+    if (!has_item) continue;
+    if (!in_path) {
+      start_sample(P, ps, it.pxy & 0xFFFFu, it.pxy >> 16, it.sample);
+      in_path = true;
+    }
+    const uint32_t nodes_before = cn.nodes;
+    const bool done = segment<CULL, FULL, COUNT, FAST>(P, nodes, prims, ps, cn, nullptr);
+    if constexpr (COUNT) seg_nodes = cn.nodes - nodes_before;
+    if (ps.traced) n_seg++;
+    if (done) {
+      in_path = false;
+      finish_sample(P, it, sum, ps.rad, scale, has_item, n_samples, n_pixels);
+    }
+  }
+  flush_stats(P, n_seg, n_samples, n_pixels, cn, COUNT);
+}
+
+/* One node of the BASIC world walk (spheres and moving spheres under boxes; trace() restricted).
+ * Both 16-B halves of the node are loaded and the box tested for every node kind (a PRIM node's box
+ * result is ignored), so the only divergent branch is the primitive test. */
+template <int CULL, bool COUNT>
+__device__ __forceinline__ void basic_step(const KParams& P, const G::Node* __restrict__ nodes,
+                                           const G::Prim* __restrict__ prims, uint32_t& i, const TRay& r,
+                                           float& closest, uint32_t& winner, Counts& cn) {
+  const G::Node* np = nodes + i;
+  const float4 a = ld4(np->mn);
+  const float4 b = ld4(np->mx);
+  const uint32_t kp = __float_as_uint(b.w);
+  const uint32_t kind = (kp >> 24) & G::KIND_MASK;
+  const float tmin = P.t_min;
+  if constexpr (COUNT) cn.nodes++;
+  const bool pass = box_hit<CULL>(a, b, r, tmin, closest, (kp & G::NODE_REF_ONLY) != 0) || kind == G::K_PRIM;
+  i = pass ? i + 1 : __float_as_uint(a.w);
+  const bool test = pass && kind != G::K_BOX;
+  if constexpr (COUNT) cn.prim_slots += __any(test) ? 1u : 0u;
+  if (test) {
+    const uint32_t payload = kp & 0xFFFFFFu;
+    const G::Prim* pp = prims + payload;
+    if constexpr (COUNT) cn.prims++;
+    float t;
+    if (sphere_root(pp, pp->km & 3u, r, tmin, closest, t, P.motion_uniform != 0)) {
+      closest = t;
+      winner = payload;
+    }
+  }
+}
+
+/* The BASIC kernel (sphere scenes: the Random family), with POSTPONED shading.  A lane's walk state
+ * (node, closest, winner, ray) lives across passes: the wave steps the walks of all its lanes one
+ * node at a time and leaves the node loop only when at least P.postpone lanes have finished theirs
+ * (or none is still walking); those lanes shade, start their next segment or sample, and the wave
+ * goes back to stepping.  Every lane still runs exactly the reference's sequence of world.hit calls
+ * and draws, so the image is the same as render_kernel's; only the wave's SIMD occupancy changes
+ * (a wave no longer idles on its slowest lane's walk before every shading step). */
+#ifndef HRT_WALK_UNROLL
+#define HRT_WALK_UNROLL 2
+#endif
+constexpr int WALK_UNROLL = HRT_WALK_UNROLL; /* node steps between two checks of the wave's exit test */
+#ifndef HRT_BASIC_WAVES
+#define HRT_BASIC_WAVES 6
+#endif
+/* waves per SIMD of the sphere-scene kernel: caps its VGPRs at 512 / waves (granule 8); with the
+ * scene in LDS two workgroups share a CU, so a workgroup is 128 * waves
+ * threads (4 SIMDs x waves x 64 / 2). */
+constexpr int BASIC_WAVES = HRT_BASIC_WAVES;
+template <bool LDS>
+constexpr int basic_block_threads() { return LDS ? 128 * BASIC_WAVES : 256; }
+
+template <int CULL, bool COUNT, bool LDS>
+__global__ __launch_bounds__(basic_block_threads<LDS>(), BASIC_WAVES)
+void render_basic_kernel(KParams P) {
+  extern __shared__ float4 lds_scene[];
+  const G::Node* nodes = P.nodes;
+  const G::Prim* prims = P.prims;
+  if constexpr (LDS) stage_scene(P, lds_scene, nodes, prims);
+  const uint32_t lane = threadIdx.x & 63u;
+  const float scale = 1.0f / (float)P.spp; /* application.rs:403 */
+  const float inf = __uint_as_float(0x7f800000u);
+  const uint32_t end = P.main_end;
+  const uint32_t need = P.postpone;
+
+  bool has_item = false, exhausted = false;
+  bool walking = false; /* a segment is in flight (walk running, or finished and waiting to shade) */
+  Item it{0u, 0u, 0u, 0u, 0u};
+  Vec3 sum = v3(0.0f, 0.0f, 0.0f);
+  PathState ps;
+  init_path_state(ps);
+  TRay r;
+  set_ray(r, ps.ro, ps.rd, 0.0f, P);
+  uint32_t node = G::NONE, winner = G::NONE;
+  float closest = inf;
+  uint32_t n_seg = 0, n_samples = 0, n_pixels = 0; /* wave totals (uniform) */
+  Counts cn{0u, 0u, 0u, 0u, 0u, 0u};
+
+  for (;;) {
+    /* lanes without work claim it; lanes with work but no segment in flight start a sample */
+    claim_work(P, lane, has_item, exhausted, it);
+    if (!__any(has_item || !exhausted)) break;
+    if (has_item && !walking) {
+      start_sample(P, ps, it.pxy & 0xFFFFu, it.pxy >> 16, it.sample);
+      walking = true;
+      set_ray(r, ps.ro, ps.rd, ps.rtime, P);
+      closest = inf;
+      winner = G::NONE;
+      node = ps.depth_left == 0 ? G::NONE : 0u; /* max_depth 0: black without a world.hit (:478-480) */
+    }
+    /* step the walks until enough lanes have finished (lanes not walking hold node >= end) */
+    if constexpr (COUNT) cn.shade_slots++;
+    const unsigned long long walkers = __ballot(walking);
+    for (;;) {
+#pragma unroll
+      for (int u = 0; u < WALK_UNROLL; u++) {
+        if constexpr (COUNT) cn.walk_slots++;
+        if (node < end) basic_step<CULL, COUNT>(P, nodes, prims, node, r, closest, winner, cn);
+      }
+      const unsigned long long live = __ballot(node < end);
+      if (!live || (uint32_t)__popcll(walkers & ~live) >= need) break;
+    }
+    /* shade the finished segments (application.rs:483-494) */
+    const bool shading = walking && node >= end;
+    const bool traced = shading && node != G::NONE;
+    bool sample_done = false, chunk_done = false;
+    if (shading) {
+      const bool done =
+          !traced || shade<false, COUNT>(P, ps, winner, closest, r.o, r.d, r.time, r.tau, cn) || ps.depth_left == 0;
+      if (done) {
+        /* application.rs:448: samples of a chunk summed in order */
+        walking = false;
+        node = G::NONE;
+        sum = sum + ps.rad;
+        sample_done = true;
+        if (++it.sample == min(P.spp, (it.chunk + 1u) * P.chunk)) {
+          if (P.n_chunks == 1) /* sqrt(sum / spp), alpha 1 (:451-456) */
+            P.out[it.out_idx] = make_float4(sqrtf(sum.x * scale), sqrtf(sum.y * scale), sqrtf(sum.z * scale), 1.0f);
+          else
+            P.partial[(size_t)it.chunk * P.n_out + it.out_idx] = make_float4(sum.x, sum.y, sum.z, 0.0f);
+          chunk_done = true;
+          has_item = false;
+          sum = v3(0.0f, 0.0f, 0.0f);
+        }
+      } else {
+        set_dir(r, ps.ro, ps.rd); /* the scattered ray keeps the sample's shutter time */
+        closest = inf;
+        winner = G::NONE;
+        node = 0u;
+      }
+    }
+    n_seg += (uint32_t)__popcll(__ballot(traced));
+    n_samples += (uint32_t)__popcll(__ballot(sample_done));
+    n_pixels += (uint32_t)__popcll(__ballot(chunk_done && it.chunk == 0u));
+  }
+  if (lane == 0) {
+    atomicAdd(&P.stats[0], (unsigned long long)n_seg);
+    atomicAdd(&P.stats[1], (unsigned long long)n_samples);
+    atomicAdd(&P.stats[2], (unsigned long long)n_pixels);
+  }
+  if constexpr (COUNT) flush_counts(P, cn);
 }
 
 /* chunk sums -> pixel, in chunk order (fixed, so 1/2/4/8-GPU splits give identical bits);
@@ -788,6 +1018,7 @@ __global__ void math_kernel(int op, const float* x, const float* y, float* out, 
     case 4: r = ln_f(a); break;
     case 5: r = pow5_f(a); break;
     case 6: r = tan_f(a); break;
+    case 7: r = div_rn(a, b, 1.0f / b); break; /* the walk's division by dot(d, d) */
   }
   out[i] = r;
 }
@@ -830,33 +1061,52 @@ hrt_status hguard(F&& f) {
   }
 }
 
+constexpr size_t SLOT_HDR = 128; /* work counter + 9 stats words, padded */
+
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-template <int CULL, bool FULL, bool COUNT, bool LDS, bool FAST>
-int resident_grid(int device, size_t smem) {
-  static int cached[64] = {0};
-  static size_t cached_smem[64] = {0};
-  if (device >= 0 && device < 64 && cached[device] && cached_smem[device] == smem) return cached[device];
-  auto fn = render_kernel<CULL, FULL, COUNT, LDS, FAST>;
-  const int block = block_threads<LDS, FAST>();
-  if (LDS) hip_check(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem),
+/* persistent grid: as many workgroups as are co-resident on the device (cached per kernel/device) */
+int resident_grid(const void* fn, int block, int device, size_t smem, bool lds) {
+  struct Key {
+    const void* fn;
+    int device;
+    size_t smem;
+    int grid;
+  };
+  static std::mutex mu;
+  static std::vector<Key> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  for (const Key& k : cache)
+    if (k.fn == fn && k.device == device && k.smem == smem) return k.grid;
+  if (lds) hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem),
                      "hipFuncSetAttribute(LDS)");
   int per_cu = 0;
   hip_check(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block, smem),
             "hipOccupancyMaxActiveBlocksPerMultiprocessor");
   hipDeviceProp_t prop;
   hip_check(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
-  int g = std::max(1, per_cu) * prop.multiProcessorCount;
-  if (device >= 0 && device < 64) { cached[device] = g; cached_smem[device] = smem; }
+  const int g = std::max(1, per_cu) * prop.multiProcessorCount;
+  cache.push_back(Key{fn, device, smem, g});
   return g;
 }
 
 template <int CULL, bool FULL, bool COUNT, bool LDS, bool FAST>
 void launch(const KParams& kp, int device, hipStream_t stream, size_t smem) {
-  int grid = resident_grid<CULL, FULL, COUNT, LDS, FAST>(device, smem);
-  hipLaunchKernelGGL((render_kernel<CULL, FULL, COUNT, LDS, FAST>), dim3(grid), dim3(block_threads<LDS, FAST>()),
-                     LDS ? smem : 0, stream, kp);
+  const void* fn = (const void*)render_kernel<CULL, FULL, COUNT, LDS, FAST>;
+  const int block = block_threads<LDS, FAST>();
+  const int grid = resident_grid(fn, block, device, LDS ? smem : 0, LDS);
+  hipLaunchKernelGGL((render_kernel<CULL, FULL, COUNT, LDS, FAST>), dim3(grid), dim3(block), LDS ? smem : 0, stream,
+                     kp);
   hip_check(hipGetLastError(), "render_kernel launch");
+}
+
+template <int CULL, bool COUNT, bool LDS>
+void launch_basic(const KParams& kp, int device, hipStream_t stream, size_t smem) {
+  const void* fn = (const void*)render_basic_kernel<CULL, COUNT, LDS>;
+  const int block = basic_block_threads<LDS>();
+  const int grid = resident_grid(fn, block, device, LDS ? smem : 0, LDS);
+  hipLaunchKernelGGL((render_basic_kernel<CULL, COUNT, LDS>), dim3(grid), dim3(block), LDS ? smem : 0, stream, kp);
+  hip_check(hipGetLastError(), "render_basic_kernel launch");
 }
 
 /* LDS residency: the reference-order stream must fit twice per CU (two 512-thread workgroups of the
@@ -866,6 +1116,7 @@ constexpr size_t LDS_FAST_MAX = 150 * 1024;
 
 struct Plan {
   bool full, fast, lds;
+  bool general; /* sphere scene forced onto the general kernel (diagnostics: HRT_KERNEL=general) */
   int cull;
   size_t smem;
 };
@@ -885,6 +1136,8 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
   pl.smem = pl.fast ? (8 * (size_t)s->f_stream_len * sizeof(G::Node) + s->f_prims.size() * sizeof(G::Prim))
                     : (s->main_end * sizeof(G::Node) + s->g_prims.size() * sizeof(G::Prim));
   pl.lds = (flags & HRT_RENDER_NO_LDS) == 0 && !pl.full && pl.smem <= (pl.fast ? LDS_FAST_MAX : LDS_SCENE_MAX);
+  const char* k = getenv("HRT_KERNEL");
+  pl.general = k && strcmp(k, "general") == 0;
   return pl;
 }
 
@@ -894,19 +1147,35 @@ void launch_any(const hrt_scene* s, const Plan& pl, const KParams& kp, hipStream
   if (pl.fast) {
     if (pl.lds) launch<G::CULL_SLAB, false, COUNT, true, true>(kp, s->device, stream, smem);
     else launch<G::CULL_SLAB, false, COUNT, false, true>(kp, s->device, stream, 0);
+  } else if (pl.general && !pl.full) {
+    const int c = pl.cull;
+    if (c == G::CULL_EXACT) pl.lds ? launch<G::CULL_EXACT, false, COUNT, true, false>(kp, s->device, stream, smem)
+                                   : launch<G::CULL_EXACT, false, COUNT, false, false>(kp, s->device, stream, 0);
+    else if (c == G::CULL_SLAB) pl.lds ? launch<G::CULL_SLAB, false, COUNT, true, false>(kp, s->device, stream, smem)
+                                       : launch<G::CULL_SLAB, false, COUNT, false, false>(kp, s->device, stream, 0);
+    else pl.lds ? launch<G::CULL_REFERENCE, false, COUNT, true, false>(kp, s->device, stream, smem)
+                : launch<G::CULL_REFERENCE, false, COUNT, false, false>(kp, s->device, stream, 0);
   } else if (pl.cull == G::CULL_EXACT) {
     if (pl.full) launch<G::CULL_EXACT, true, COUNT, false, false>(kp, s->device, stream, 0);
-    else if (pl.lds) launch<G::CULL_EXACT, false, COUNT, true, false>(kp, s->device, stream, smem);
-    else launch<G::CULL_EXACT, false, COUNT, false, false>(kp, s->device, stream, 0);
+    else if (pl.lds) launch_basic<G::CULL_EXACT, COUNT, true>(kp, s->device, stream, smem);
+    else launch_basic<G::CULL_EXACT, COUNT, false>(kp, s->device, stream, 0);
   } else if (pl.cull == G::CULL_SLAB) {
     if (pl.full) launch<G::CULL_SLAB, true, COUNT, false, false>(kp, s->device, stream, 0);
-    else if (pl.lds) launch<G::CULL_SLAB, false, COUNT, true, false>(kp, s->device, stream, smem);
-    else launch<G::CULL_SLAB, false, COUNT, false, false>(kp, s->device, stream, 0);
+    else if (pl.lds) launch_basic<G::CULL_SLAB, COUNT, true>(kp, s->device, stream, smem);
+    else launch_basic<G::CULL_SLAB, COUNT, false>(kp, s->device, stream, 0);
   } else {
     if (pl.full) launch<G::CULL_REFERENCE, true, COUNT, false, false>(kp, s->device, stream, 0);
-    else if (pl.lds) launch<G::CULL_REFERENCE, false, COUNT, true, false>(kp, s->device, stream, smem);
-    else launch<G::CULL_REFERENCE, false, COUNT, false, false>(kp, s->device, stream, 0);
+    else if (pl.lds) launch_basic<G::CULL_REFERENCE, COUNT, true>(kp, s->device, stream, smem);
+    else launch_basic<G::CULL_REFERENCE, COUNT, false>(kp, s->device, stream, 0);
   }
+}
+
+/* BASIC-kernel tuning knob, 1..64 lanes (read per launch; any value gives the same image):
+ *   HRT_POSTPONE   a wave leaves the walk to shade once this many lanes have finished theirs. */
+uint32_t env_knob(const char* name, uint32_t dflt) {
+  const char* e = getenv(name);
+  const long x = e ? strtol(e, nullptr, 10) : 0;
+  return (uint32_t)(x >= 1 && x <= 64 ? x : dflt);
 }
 
 /* scene + camera + render knobs of a launch (work-distribution fields are set by the caller) */
@@ -944,6 +1213,10 @@ KParams scene_params(const hrt_scene* s, const hrt_camera* cam, const hrt_render
   kp.n_nodes = pl.fast ? 8 * s->f_stream_len : s->main_end;
   kp.n_prims = (uint32_t)(pl.fast ? s->f_prims.size() : s->g_prims.size());
   kp.stream_len = pl.fast ? s->f_stream_len : 0;
+  kp.postpone = env_knob("HRT_POSTPONE", 48);
+  kp.motion_uniform = s->motion_uniform ? 1u : 0u;
+  kp.motion_t0 = s->motion_t0;
+  kp.motion_span = s->motion_span;
   return kp;
 }
 
@@ -1036,7 +1309,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     if (!s || !cam || !p || !tiles || !d_rgba || n_tiles == 0)
       throw HipError{HRT_ERR_INVALID_ARG, "hrt_render_tiles_device: null argument"};
     if (!s->committed || !s->d_blob) throw HipError{HRT_ERR_STATE, "scene not committed"};
-    if (p->width < 2 || p->height < 2 || p->samples == 0 || (p->flags & ~(uint32_t)(HRT_RENDER_COUNT_WORK | HRT_RENDER_NO_LDS | HRT_RENDER_REFERENCE_CULL |
+    if (p->width < 2 || p->height < 2 || p->width > 65535 || p->height > 65535 || p->samples == 0 || (p->flags & ~(uint32_t)(HRT_RENDER_COUNT_WORK | HRT_RENDER_NO_LDS | HRT_RENDER_REFERENCE_CULL |
                                      HRT_RENDER_FAST_CULL | HRT_RENDER_SAH)) != 0)
       throw HipError{HRT_ERR_INVALID_ARG, "bad render params (width/height >= 2, samples > 0, known flags)"};
     if (!(cam->time0 < cam->time1)) throw HipError{HRT_ERR_INVALID_ARG, "camera time0 must be < time1"};
@@ -1059,7 +1332,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     if (pad >= 0xFFFF0000ull) throw HipError{HRT_ERR_UNSUPPORTED, "more than 4G pixels in one call"};
     hipStream_t stream = (hipStream_t)stream_;
     DeviceGuard dg(s->device);
-    /* scratch slot: device [counter u32 | pad | stats 3 x u64 | tiles], pinned host [stats | tiles] */
+    /* scratch slot: device [counter u32 | pad | stats 8 x u64 | pad to HDR | tiles], pinned host [stats | tiles] */
     std::lock_guard<std::mutex> lock(*static_cast<std::mutex*>(s->slot_mutex));
     hrt_scene::Slot& sl = s->slots[s->next_slot++ % hrt_scene::N_SLOTS];
     if (sl.used) hip_check(hipEventSynchronize((hipEvent_t)sl.event), "hipEventSynchronize(slot)");
@@ -1070,8 +1343,8 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
       sl.d_mem = sl.h_tiles = nullptr;
       sl.tiles_cap = 0;
       size_t cap = std::max<size_t>(tiles_bytes, 64 * sizeof(G::TileDev));
-      hip_check(hipMalloc(&sl.d_mem, 64 + cap), "hipMalloc(slot)");
-      hip_check(hipHostMalloc(&sl.h_tiles, 64 + cap, hipHostMallocDefault), "hipHostMalloc(slot)");
+      hip_check(hipMalloc(&sl.d_mem, SLOT_HDR + cap), "hipMalloc(slot)");
+      hip_check(hipHostMalloc(&sl.h_tiles, SLOT_HDR + cap, hipHostMallocDefault), "hipHostMalloc(slot)");
       sl.tiles_cap = cap;
     }
     const size_t partial_bytes = n_chunks > 1 ? (size_t)n_chunks * outp * sizeof(float4) : 0;
@@ -1083,13 +1356,13 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
       sl.partial_cap = partial_bytes;
     }
     void* scratch = sl.d_mem;
-    memcpy((uint8_t*)sl.h_tiles + 64, td.data(), tiles_bytes);
-    hip_check(hipMemsetAsync(scratch, 0, 64, stream), "hipMemsetAsync");
-    hip_check(hipMemcpyAsync((uint8_t*)scratch + 64, (uint8_t*)sl.h_tiles + 64, tiles_bytes, hipMemcpyHostToDevice,
+    memcpy((uint8_t*)sl.h_tiles + SLOT_HDR, td.data(), tiles_bytes);
+    hip_check(hipMemsetAsync(scratch, 0, SLOT_HDR, stream), "hipMemsetAsync");
+    hip_check(hipMemcpyAsync((uint8_t*)scratch + SLOT_HDR, (uint8_t*)sl.h_tiles + SLOT_HDR, tiles_bytes, hipMemcpyHostToDevice,
                              stream), "hipMemcpyAsync(tiles)");
     const Plan pl = plan(s, cam, p->flags);
     KParams kp = scene_params(s, cam, p, pl);
-    kp.tiles = (const G::TileDev*)((uint8_t*)scratch + 64);
+    kp.tiles = (const G::TileDev*)((uint8_t*)scratch + SLOT_HDR);
     kp.n_tiles = n_tiles;
     kp.total_work = (uint32_t)pad;
     kp.out = (float4*)d_rgba;
@@ -1108,7 +1381,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
       hip_check(hipGetLastError(), "reduce_chunks launch");
     }
     unsigned long long* h = (unsigned long long*)sl.h_tiles;
-    if (stats) hip_check(hipMemcpyAsync(h, (uint8_t*)scratch + 8, 48, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(stats)");
+    if (stats) hip_check(hipMemcpyAsync(h, (uint8_t*)scratch + 8, 72, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(stats)");
     hip_check(hipEventRecord((hipEvent_t)sl.event, stream), "hipEventRecord(slot)");
     sl.used = true;
     if (stats) {
@@ -1119,6 +1392,9 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
       stats->node_visits = h[3];
       stats->prim_tests = h[4];
       stats->tex_evals = h[5];
+      stats->walk_slots = h[6];
+      stats->shade_slots = h[7];
+      stats->prim_slots = h[8];
     }
   });
 }
@@ -1192,7 +1468,7 @@ hrt_status hrt_debug_trace_path(hrt_scene* s, const hrt_camera* cam, const hrt_r
 
 hrt_status hrt_debug_device_math(int32_t op, const float* x, const float* y, float* out, uint32_t n) {
   return hguard([&] {
-    if (!x || !out || op < 0 || op > 6) throw HipError{HRT_ERR_INVALID_ARG, "bad argument"};
+    if (!x || !out || op < 0 || op > 7) throw HipError{HRT_ERR_INVALID_ARG, "bad argument"};
     if (n == 0) return;
     float *dx = nullptr, *dy = nullptr, *dout = nullptr;
     hip_check(hipMalloc((void**)&dx, n * 4), "hipMalloc");

@@ -571,12 +571,26 @@ void flatten(hrt_scene* s) {
     s->g_media[f.pending[i].medium].bend = (uint32_t)s->g_nodes.size();
   }
   for (const G::Medium& m : s->g_media) s->feature_mask |= tex_features(s, s->g_mats[m.mat].tex);
-  /* A slab test only culls subtrees no accepted hit can come from when every box contains its
-   * geometry; rect boxes do not (ZX swap, edge-on faces) and instances/media change the ray, so
-   * those scenes keep the reference's per-axis test ("culling"). */
+  /* Default culling: the reference's per-axis test AND the provably safe inflated slab test
+   * (layout.h CULL_EXACT; boxes that may not hold their geometry are flagged NODE_REF_ONLY). */
   bool sphere_only = (s->feature_mask & (G::F_RECT | G::F_INSTANCE | G::F_MEDIUM)) == 0;
   s->cull_mode = G::CULL_EXACT;
   s->ln_e = ln_f(E_F);
+  /* moving_sphere.rs:55-58 divides by (time1 - time0) per call; when every moving sphere has the
+   * same time0 and time1 (all reference scenes) the quotient depends on the ray only */
+  s->motion_uniform = true;
+  bool first = true;
+  for (const G::Prim& p : s->g_prims) {
+    if ((p.km & 3u) != G::P_MOVING) continue;
+    if (first) {
+      s->motion_t0 = p.p1[3];
+      s->motion_span = p.p2[0];
+      first = false;
+    } else if (memcmp(&s->motion_t0, &p.p1[3], 4) != 0 || memcmp(&s->motion_span, &p.p2[0], 4) != 0) {
+      s->motion_uniform = false;
+    }
+  }
+  if (first) s->motion_uniform = false; /* no moving sphere */
   s->f_nodes.clear();
   s->f_prims.clear();
   s->f_stream_len = 0;

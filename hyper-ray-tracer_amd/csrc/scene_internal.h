@@ -96,6 +96,8 @@ struct hrt_scene {
   float box_t0 = -3.40282347e+38f;  /* every BVH box is valid for ray times in [box_t0, box_t1] */
   float box_t1 = 3.40282347e+38f;
   float ln_e = 0; /* ln(E) as computed by hd_math (constant_medium.rs:59) */
+  bool motion_uniform = false; /* every moving sphere shares (time0, time1 - time0) */
+  float motion_t0 = 0, motion_span = 1;
 
   /* ---- device ---- */
   int device = -1;

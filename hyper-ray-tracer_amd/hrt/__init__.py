@@ -82,7 +82,8 @@ class Tile(ctypes.Structure):
 
 
 class RenderStats(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_uint64) for n in ("segments", "samples", "pixels", "node_visits", "prim_tests", "tex_evals")]
+    _fields_ = [(n, ctypes.c_uint64) for n in ("segments", "samples", "pixels", "node_visits", "prim_tests", "tex_evals",
+                                                      "walk_slots", "shade_slots", "prim_slots")]
 
 
 class PresetInfo(ctypes.Structure):

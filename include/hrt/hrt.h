@@ -101,6 +101,11 @@ typedef struct hrt_render_stats {
   uint64_t node_visits;     /* HRT_RENDER_COUNT_WORK only: node-stream entries read */
   uint64_t prim_tests;      /* HRT_RENDER_COUNT_WORK only: primitive intersection tests */
   uint64_t tex_evals;       /* HRT_RENDER_COUNT_WORK only: Texture::value evaluations */
+  uint64_t walk_slots;      /* HRT_RENDER_COUNT_WORK only: 64 x wave iterations of the node walk
+                               (node_visits / walk_slots = SIMD lane utilisation of the walk) */
+  uint64_t shade_slots;     /* HRT_RENDER_COUNT_WORK only: 64 x wave passes through shading */
+  uint64_t prim_slots;      /* HRT_RENDER_COUNT_WORK only: 64 x wave runs of the primitive block
+                               (sphere-scene kernel; 0 for the general kernel) */
 } hrt_render_stats;
 
 /* Scene description of one reference preset (application.rs:132-211). */

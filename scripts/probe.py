@@ -18,6 +18,8 @@ ap.add_argument("--spp", type=int, default=16)
 ap.add_argument("--depth", type=int, default=50)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--ab", default="", help="comma list of flag values to alternate (A/B in one process)")
+ap.add_argument("--env", default="", help="/-list of NAME=VALUE[,NAME=VALUE] env settings to alternate (A/B)")
+ap.add_argument("--count", action="store_true", help="also run one instrumented pass per variant")
 a = ap.parse_args()
 
 s = hrt.preset(a.preset, 1)
@@ -26,23 +28,48 @@ si = s.scene_info()
 print(f"scene {a.preset}: nodes {si.nodes} prims {si.prims} features {si.feature_mask:#x} cull {si.cull_mode} blob {si.blob_bytes} B", flush=True)
 cam = hrt.preset_camera(s.info, a.width, a.height)
 flag_sets = [int(x) for x in a.ab.split(",")] if a.ab else [0]
+env_sets = a.env.split("/") if a.env else [""]
+flag_sets = [(f, e) for f in flag_sets for e in env_sets]
+
+
+def set_env(e):
+    for kv in filter(None, e.split(",")):
+        k, v = kv.split("=", 1)
+        os.environ[k] = v
+
+
+def clear_env(e):
+    for kv in filter(None, e.split(",")):
+        os.environ.pop(kv.split("=", 1)[0], None)
 out = torch.empty((a.height, a.width, 4), dtype=torch.float32, device="cuda")
 tiles = [(0, 0, a.width, a.height)]
-res = {f: [] for f in flag_sets}
+res = {k: [] for k in flag_sets}
 imgs = {}
 for r in range(a.reps):
-    for fl in flag_sets:
+    for key in flag_sets:
+        fl, env = key
+        set_env(env)
         p = hrt.params(a.width, a.height, a.spp, a.depth, 1, tuple(s.info.background), flags=fl)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         st = hrt.render_tiles_device(s, cam, p, tiles, out.data_ptr(), 0, want_stats=True)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        res[fl].append(st.segments / dt / 1e6)
-        imgs[fl] = out.clone()
-        print(f"rep {r} flags {fl}: {dt*1e3:.1f} ms  segments {st.segments}  seg/sample {st.segments/st.samples:.3f}  "
+        res[key].append(st.segments / dt / 1e6)
+        imgs[key] = out.clone()
+        clear_env(env)
+        print(f"rep {r} {key}: {dt*1e3:.1f} ms  segments {st.segments}  seg/sample {st.segments/st.samples:.3f}  "
               f"{st.segments/dt/1e6:.1f} Mrays/s  {st.samples/dt/1e6:.1f} Msamples/s", flush=True)
-for fl in flag_sets:
-    print(f"flags {fl}: median {sorted(res[fl])[len(res[fl])//2]:.1f} Mrays/s  identical-to-first {bool(torch.equal(imgs[fl], imgs[flag_sets[0]]))}")
+for key in flag_sets:
+    print(f"{key}: median {sorted(res[key])[len(res[key])//2]:.1f} Mrays/s  identical-to-first {bool(torch.equal(imgs[key], imgs[flag_sets[0]]))}")
+    if a.count:
+        fl, env = key
+        set_env(env)
+        p = hrt.params(a.width, a.height, a.spp, a.depth, 1, tuple(s.info.background), flags=fl | hrt.RENDER_COUNT_WORK)
+        st = hrt.render_tiles_device(s, cam, p, tiles, out.data_ptr(), 0, want_stats=True)
+        clear_env(env)
+        print(f"   count: nodes/ray {st.node_visits/st.segments:.2f} prims/ray {st.prim_tests/st.segments:.3f} "
+              f"walk-lane-util {st.node_visits/max(1, st.walk_slots):.3f} walk-iters/ray {st.walk_slots/st.segments:.1f} "
+              f"shade-passes/ray {st.shade_slots/st.segments:.3f} prim-blocks/ray {st.prim_slots/st.segments:.2f} (x64 lanes)", flush=True)
 img = out.cpu().numpy()
 print("mean rgb", img[..., :3].mean(axis=(0, 1)), "finite", bool(np.isfinite(img).all()))

@@ -1,0 +1,42 @@
+/* Exhaustive-style check of the kernel's division by dot(d, d) (render.hip div_rn): the fma-corrected
+ * quotient with a per-ray RN(1/a) must equal IEEE x / a bit for bit wherever the fast path is taken.
+ * Usage: div_rn_check <n> <seed> <emin> <emax>   prints "<fast-path cases> <mismatches>". */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+static float f(uint32_t u) { float x; memcpy(&x, &u, 4); return x; }
+static uint32_t u(float x) { uint32_t v; memcpy(&v, &x, 4); return v; }
+
+int main(int argc, char** argv) {
+  if (argc < 5) return 2;
+  long n = atol(argv[1]);
+  uint64_t s = strtoull(argv[2], 0, 10) * 0x9E3779B97F4A7C15ull + 1;
+  int emin = atoi(argv[3]), emax = atoi(argv[4]);
+  long fast = 0, bad = 0;
+  for (long i = 0; i < n; i++) {
+    s ^= s << 13; s ^= s >> 7; s ^= s << 17;
+    uint64_t r = s;
+    int ea = emin + (int)((r >> 40) % (uint64_t)(emax - emin + 1));
+    int ex = emin + (int)((r >> 50) % (uint64_t)(emax - emin + 1));
+    uint32_t ma = (uint32_t)r & 0x7fffff, mx = (uint32_t)(r >> 23) & 0x7fffff;
+    if ((i & 7) == 0) ma = 0x7fffff;  /* significands of all ones: the hard reciprocals */
+    if ((i & 15) == 1) mx = 0x7fffff;
+    if ((i & 31) == 2) ma = 0;
+    float a = f(((uint32_t)(ea + 127) << 23) | ma);
+    float x = f(((uint32_t)(ex + 127) << 23) | mx | (uint32_t)((r >> 63) << 31));
+    volatile float yv = 1.0f / a, qv = x / a;
+    float y = yv, q = qv;
+    float q0 = x * y;
+    float ax = fabsf(x), aq = fabsf(q0);
+    if (!(ax >= 0x1p-100f && ax <= 0x1p100f && aq >= 0x1p-100f && aq <= 0x1p100f && a >= 0x1p-100f && a <= 0x1p100f))
+      continue;
+    fast++;
+    float got = fmaf(fmaf(-q0, a, x), y, q0);
+    if (u(got) != u(q)) bad++;
+  }
+  printf("%ld %ld\n", fast, bad);
+  return 0;
+}
