@@ -83,6 +83,13 @@ struct Counts {
   uint32_t prim_slots;              /* lane slots of wave executions of the primitive block */
 };
 
+/* COUNT builds of the sphere-scene kernel: shader-clock cycles per wave phase (s_memtime stamps,
+ * uniform per wave): [0] claim + sample start, [1] walk, [2] shading */
+struct PhaseClock {
+  unsigned long long cyc[3];
+  unsigned long long last;
+};
+
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
   for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
   return v;
@@ -512,6 +519,35 @@ __device__ float perlin_noise(const G::Perlin* pn, Vec3 point) {
   return acc;
 }
 
+/* sign of sin_f(v) for 1e-6 <= |v| <= 1e6: sin_f reduces v by pi/2 (hd_math reduce_pio2, same
+ * operations here) and returns sin_poly(r) / cos_poly(r) / -sin_poly(r) / -cos_poly(r) by quadrant;
+ * for |r| < 1 sin_poly keeps the sign of r and cos_poly is positive, so only the reduction is needed.
+ * (|n| < 2^20: rint is exact and n & 3 is reduce_pio2's quadrant.) */
+__device__ __forceinline__ bool sin_negative(float vf) {
+  const double x = (double)vf;
+  const double n = __builtin_rint(x * detail::TWO_OVER_PI);
+  const double r = ((x - n * detail::P1) - n * detail::P2) - n * detail::P3;
+  const int q = (int)n & 3;
+  return q == 3 || (q == 0 && r < 0.0) || (q == 2 && r > 0.0);
+}
+
+/* the full product, as the oracle computes it; a real call, so that its f64 temporaries do not
+ * count towards the registers of the kernels it is reached from (it runs only for rare inputs) */
+__device__ __attribute__((noinline)) bool checker_product_negative(float vx, float vy, float vz) {
+  return (sin_f(vx) * sin_f(vy)) * sin_f(vz) < 0.0f;
+}
+
+/* checker_texture.rs:22-29: sin(10x) * sin(10y) * sin(10z) < 0, decided from the signs.  With every
+ * |v| in [1e-6, 1e6] each f32 sine is nonzero (an f32 there is > 1e-9 from any multiple of pi) and the
+ * product of three cannot underflow, so the product is negative exactly when an odd number of
+ * factors are; anything else (zero, tiny, huge, NaN) takes sin_f's full product. */
+__device__ __forceinline__ bool checker_odd(float vx, float vy, float vz) {
+  const float ax = fabsf(vx), ay = fabsf(vy), az = fabsf(vz);
+  const bool in_range = ax >= 1e-6f && ax <= 1e6f && ay >= 1e-6f && ay <= 1e6f && az >= 1e-6f && az <= 1e6f;
+  if (in_range) return sin_negative(vx) != (sin_negative(vy) != sin_negative(vz));
+  return checker_product_negative(vx, vy, vz);
+}
+
 /* textures/.rs value() */
 template <bool FULL, bool COUNT>
 __device__ Vec3 tex_value(const KParams& P, uint32_t id, float u, float v, Vec3 p, Counts& cn) {
@@ -520,8 +556,7 @@ __device__ Vec3 tex_value(const KParams& P, uint32_t id, float u, float v, Vec3 
     if constexpr (COUNT) cn.tex++;
     if (T.kind == G::T_SOLID) return v3(T.a[0], T.a[1], T.a[2]);
     if (T.kind == G::T_CHECKER) { /* checker_texture.rs:22-29 */
-      float sines = sin_f(10.0f * p.x) * sin_f(10.0f * p.y) * sin_f(10.0f * p.z);
-      id = sines < 0.0f ? T.i0 : T.i1;
+      id = checker_odd(10.0f * p.x, 10.0f * p.y, 10.0f * p.z) ? T.i0 : T.i1;
       continue;
     }
     if constexpr (FULL) {
@@ -924,6 +959,15 @@ void render_basic_kernel(KParams P) {
   float closest = inf;
   uint32_t n_seg = 0, n_samples = 0, n_pixels = 0; /* wave totals (uniform) */
   Counts cn{0u, 0u, 0u, 0u, 0u, 0u};
+  PhaseClock pc{{0ull, 0ull, 0ull}, 0ull};
+  auto stamp = [&](int phase) {
+    if constexpr (COUNT) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (phase >= 0) pc.cyc[phase] += t - pc.last;
+      pc.last = t;
+    }
+  };
+  stamp(-1);
 
   for (;;) {
     /* lanes without work claim it; lanes with work but no segment in flight start a sample */
@@ -939,6 +983,7 @@ void render_basic_kernel(KParams P) {
     }
     /* step the walks until enough lanes have finished (lanes not walking hold node >= end) */
     if constexpr (COUNT) cn.shade_slots++;
+    stamp(0);
     const unsigned long long walkers = __ballot(walking);
     for (;;) {
 #pragma unroll
@@ -949,6 +994,7 @@ void render_basic_kernel(KParams P) {
       const unsigned long long live = __ballot(node < end);
       if (!live || (uint32_t)__popcll(walkers & ~live) >= need) break;
     }
+    stamp(1);
     /* shade the finished segments (application.rs:483-494) */
     const bool shading = walking && node >= end;
     const bool traced = shading && node != G::NONE;
@@ -981,13 +1027,18 @@ void render_basic_kernel(KParams P) {
     n_seg += (uint32_t)__popcll(__ballot(traced));
     n_samples += (uint32_t)__popcll(__ballot(sample_done));
     n_pixels += (uint32_t)__popcll(__ballot(chunk_done && it.chunk == 0u));
+    stamp(2);
   }
   if (lane == 0) {
     atomicAdd(&P.stats[0], (unsigned long long)n_seg);
     atomicAdd(&P.stats[1], (unsigned long long)n_samples);
     atomicAdd(&P.stats[2], (unsigned long long)n_pixels);
   }
-  if constexpr (COUNT) flush_counts(P, cn);
+  if constexpr (COUNT) {
+    flush_counts(P, cn);
+    if (lane == 0)
+      for (int k = 0; k < 3; k++) atomicAdd(&P.stats[9 + k], pc.cyc[k]);
+  }
 }
 
 /* chunk sums -> pixel, in chunk order (fixed, so 1/2/4/8-GPU splits give identical bits);
@@ -1061,7 +1112,7 @@ hrt_status hguard(F&& f) {
   }
 }
 
-constexpr size_t SLOT_HDR = 128; /* work counter + 9 stats words, padded */
+constexpr size_t SLOT_HDR = 128; /* work counter + 12 stats words, padded */
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -1213,7 +1264,7 @@ KParams scene_params(const hrt_scene* s, const hrt_camera* cam, const hrt_render
   kp.n_nodes = pl.fast ? 8 * s->f_stream_len : s->main_end;
   kp.n_prims = (uint32_t)(pl.fast ? s->f_prims.size() : s->g_prims.size());
   kp.stream_len = pl.fast ? s->f_stream_len : 0;
-  kp.postpone = env_knob("HRT_POSTPONE", 48);
+  kp.postpone = env_knob("HRT_POSTPONE", 60);
   kp.motion_uniform = s->motion_uniform ? 1u : 0u;
   kp.motion_t0 = s->motion_t0;
   kp.motion_span = s->motion_span;
@@ -1381,7 +1432,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
       hip_check(hipGetLastError(), "reduce_chunks launch");
     }
     unsigned long long* h = (unsigned long long*)sl.h_tiles;
-    if (stats) hip_check(hipMemcpyAsync(h, (uint8_t*)scratch + 8, 72, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(stats)");
+    if (stats) hip_check(hipMemcpyAsync(h, (uint8_t*)scratch + 8, 96, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(stats)");
     hip_check(hipEventRecord((hipEvent_t)sl.event, stream), "hipEventRecord(slot)");
     sl.used = true;
     if (stats) {
@@ -1395,6 +1446,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
       stats->walk_slots = h[6];
       stats->shade_slots = h[7];
       stats->prim_slots = h[8];
+      for (int k = 0; k < 3; k++) stats->phase_cycles[k] = h[9 + k];
     }
   });
 }

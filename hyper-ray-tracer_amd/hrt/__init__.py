@@ -83,7 +83,8 @@ class Tile(ctypes.Structure):
 
 class RenderStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in ("segments", "samples", "pixels", "node_visits", "prim_tests", "tex_evals",
-                                                      "walk_slots", "shade_slots", "prim_slots")]
+                                                      "walk_slots", "shade_slots", "prim_slots")] + \
+        [("phase_cycles", ctypes.c_uint64 * 3)]
 
 
 class PresetInfo(ctypes.Structure):

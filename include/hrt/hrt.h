@@ -106,6 +106,8 @@ typedef struct hrt_render_stats {
   uint64_t shade_slots;     /* HRT_RENDER_COUNT_WORK only: 64 x wave passes through shading */
   uint64_t prim_slots;      /* HRT_RENDER_COUNT_WORK only: 64 x wave runs of the primitive block
                                (sphere-scene kernel; 0 for the general kernel) */
+  uint64_t phase_cycles[3]; /* HRT_RENDER_COUNT_WORK, sphere-scene kernel: shader cycles summed over
+                               waves spent in [0] work claim + sample start, [1] walk, [2] shading */
 } hrt_render_stats;
 
 /* Scene description of one reference preset (application.rs:132-211). */

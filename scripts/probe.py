@@ -71,5 +71,8 @@ for key in flag_sets:
         print(f"   count: nodes/ray {st.node_visits/st.segments:.2f} prims/ray {st.prim_tests/st.segments:.3f} "
               f"walk-lane-util {st.node_visits/max(1, st.walk_slots):.3f} walk-iters/ray {st.walk_slots/st.segments:.1f} "
               f"shade-passes/ray {st.shade_slots/st.segments:.3f} prim-blocks/ray {st.prim_slots/st.segments:.2f} (x64 lanes)", flush=True)
+        pcs = list(st.phase_cycles)
+        if sum(pcs):
+            print("   phase cycles: claim+start {:.1%}  walk {:.1%}  shade {:.1%}".format(*[c / sum(pcs) for c in pcs]), flush=True)
 img = out.cpu().numpy()
 print("mean rgb", img[..., :3].mean(axis=(0, 1)), "finite", bool(np.isfinite(img).all()))

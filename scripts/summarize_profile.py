@@ -32,8 +32,8 @@ def per_dispatch(rs):
     return out
 
 
-def is_main(name):
-    return "render_kernel" in name and "true, true>" not in name and ", true>" not in name.split("render_kernel")[1][:25]
+def is_render(name):
+    return "render_kernel" in name or "render_basic_kernel" in name
 
 
 lines = [f"# rocprofv3 summary `{tag}`: bench.py, {preset} {W}x{H} {spp} spp\n"]
@@ -44,12 +44,12 @@ if os.path.exists(kt):
     for r in csv.DictReader(open(kt)):
         lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs'])/1e6:.3f} | {float(r['TotalDurationNs'])/1e6:.3f} |")
 fetch, write, sq = per_dispatch(rows("fetch")), per_dispatch(rows("write")), per_dispatch(rows("sq"))
-main_f = [v for (d, n), v in sorted(fetch.items()) if "render_kernel" in n]
-main_w = [v for (d, n), v in sorted(write.items()) if "render_kernel" in n]
-main_sq = [(n, v) for (d, n), v in sorted(sq.items()) if "render_kernel" in n]
+main_f = [v for (d, n), v in sorted(fetch.items()) if is_render(n)]
+main_w = [v for (d, n), v in sorted(write.items()) if is_render(n)]
+main_sq = [(n, v) for (d, n), v in sorted(sq.items()) if is_render(n)]
 traffic = None
 if main_f and main_w:
-    # the first render_kernel dispatch of the run is the timed kernel's twin (stats warm-up)
+    # the first render dispatch of the run is the timed kernel's twin (stats warm-up)
     f_kb, w_kb = main_f[0].get("FETCH_SIZE", 0.0), main_w[0].get("WRITE_SIZE", 0.0)
     traffic = int(2 * f_kb * 1024 + w_kb * 1024)
     lines.append(f"\n## HBM traffic per launch (PMC, separate passes)\n\nFETCH_SIZE {f_kb:.0f} KB (x2 gfx950 correction), "
@@ -57,7 +57,7 @@ if main_f and main_w:
 if main_sq:
     n, v = main_sq[0]
     waves = v.get("SQ_WAVES", 0)
-    lines.append("## SQ counters (first render_kernel dispatch)\n")
+    lines.append("## SQ counters (first render dispatch)\n")
     for k in sorted(v):
         lines.append(f"- {k}: {v[k]:.4g}")
     if v.get("GRBM_GUI_ACTIVE") and v.get("SQ_INSTS_VALU"):
