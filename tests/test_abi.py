@@ -170,3 +170,15 @@ def test_device_info_needs_commit():
     with pytest.raises(hrt.HrtError) as e:
         s.scene_info()
     assert e.value.status == hrt.ERR_STATE
+
+
+def test_commit_without_a_device_fails_loudly():
+    """No CPU fallback: on a host without a GPU the device upload (and so every render) is an error."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    s = hrt.preset("two_spheres", 1)
+    with pytest.raises(hrt.HrtError) as e:
+        s.commit(0)
+    assert e.value.status == hrt.ERR_HIP
