@@ -591,6 +591,8 @@ void flatten(hrt_scene* s) {
     }
   }
   if (first) s->motion_uniform = false; /* no moving sphere */
+  s->media_nested = false;
+  for (const G::Medium& m : s->g_media) s->media_nested |= m.parent != G::NONE;
   s->f_nodes.clear();
   s->f_prims.clear();
   s->f_stream_len = 0;
@@ -598,6 +600,48 @@ void flatten(hrt_scene* s) {
 }
 
 }  // namespace
+
+namespace hrt {
+void flatten_scene(hrt_scene* s) { flatten(s); }
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+/* one blob per device: every layout.h section 256-B aligned */
+std::vector<uint8_t> build_blob(hrt_scene* s) {
+  size_t off = 0;
+  auto section = [&](size_t bytes) {
+    size_t o = off;
+    off = align256(off + std::max<size_t>(bytes, 16));
+    return o;
+  };
+  s->off_nodes = section(s->g_nodes.size() * sizeof(G::Node));
+  s->off_prims = section(s->g_prims.size() * sizeof(G::Prim));
+  s->off_insts = section(s->g_insts.size() * sizeof(G::Inst));
+  s->off_media = section(s->g_media.size() * sizeof(G::Medium));
+  s->off_mats = section(s->g_mats.size() * sizeof(G::Mat));
+  s->off_texs = section(s->g_texs.size() * sizeof(G::Tex));
+  s->off_perlin = section(s->perlin.size() * sizeof(G::Perlin));
+  s->off_images = section(s->images.size());
+  s->off_fnodes = section(s->f_nodes.size() * sizeof(G::Node));
+  s->off_fprims = section(s->f_prims.size() * sizeof(G::Prim));
+  s->blob_bytes = off;
+  std::vector<uint8_t> blob(off, 0);
+  auto put = [&](size_t o, const void* src, size_t bytes) {
+    if (bytes) memcpy(blob.data() + o, src, bytes);
+  };
+  put(s->off_nodes, s->g_nodes.data(), s->g_nodes.size() * sizeof(G::Node));
+  put(s->off_prims, s->g_prims.data(), s->g_prims.size() * sizeof(G::Prim));
+  put(s->off_insts, s->g_insts.data(), s->g_insts.size() * sizeof(G::Inst));
+  put(s->off_media, s->g_media.data(), s->g_media.size() * sizeof(G::Medium));
+  put(s->off_mats, s->g_mats.data(), s->g_mats.size() * sizeof(G::Mat));
+  put(s->off_texs, s->g_texs.data(), s->g_texs.size() * sizeof(G::Tex));
+  put(s->off_perlin, s->perlin.data(), s->perlin.size() * sizeof(G::Perlin));
+  put(s->off_images, s->images.data(), s->images.size());
+  put(s->off_fnodes, s->f_nodes.data(), s->f_nodes.size() * sizeof(G::Node));
+  put(s->off_fprims, s->f_prims.data(), s->f_prims.size() * sizeof(G::Prim));
+  return blob;
+}
+}  // namespace hrt
 
 /* ============================================================================ C ABI */
 extern "C" {
@@ -968,6 +1012,39 @@ hrt_status hrt_scene_get_info(const hrt_scene* s, hrt_scene_info* info) {
     info->sah_stream_len = s->f_stream_len;
     if (s->f_stream_len) /* the plan the renderer uses for a [0,1] shutter (render.hip plan()) */
       info->in_lds = 8 * s->f_stream_len * sizeof(G::Node) + s->f_prims.size() * sizeof(G::Prim) <= 150 * 1024 ? 1u : 0u;
+  });
+}
+
+/* Flatten without a device (tests/native/lane_sim.hip runs the kernels' per-lane code on it). */
+hrt_status hrt_debug_scene_blob(hrt_scene* s, void* out, uint64_t cap, uint64_t* size, hrt_blob_info* info) {
+  return guard([&] {
+    need(s && size, HRT_ERR_INVALID_ARG, "bad argument");
+    need(s->root != G::NONE, HRT_ERR_STATE, "no root set");
+    if (!s->committed) flatten(s);
+    std::vector<uint8_t> blob = build_blob(s);
+    *size = blob.size();
+    if (out) {
+      need(cap >= blob.size(), HRT_ERR_INVALID_ARG, "buffer too small");
+      memcpy(out, blob.data(), blob.size());
+    }
+    if (info) {
+      memset(info, 0, sizeof(*info));
+      info->off_nodes = s->off_nodes; info->off_prims = s->off_prims; info->off_insts = s->off_insts;
+      info->off_media = s->off_media; info->off_mats = s->off_mats; info->off_texs = s->off_texs;
+      info->off_perlin = s->off_perlin; info->off_images = s->off_images;
+      info->n_nodes = (uint32_t)s->g_nodes.size();
+      info->main_end = s->main_end;
+      info->n_prims = (uint32_t)s->g_prims.size();
+      info->feature_mask = s->feature_mask;
+      info->cull_mode = (uint32_t)s->cull_mode;
+      info->motion_uniform = s->motion_uniform ? 1u : 0u;
+      info->motion_t0 = s->motion_t0;
+      info->motion_span = s->motion_span;
+      info->ln_e = s->ln_e;
+      info->media_nested = s->media_nested ? 1u : 0u;
+      info->box_t0 = s->box_t0;
+      info->box_t1 = s->box_t1;
+    }
   });
 }
 

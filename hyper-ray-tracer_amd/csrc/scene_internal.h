@@ -97,6 +97,7 @@ struct hrt_scene {
   float box_t1 = 3.40282347e+38f;
   float ln_e = 0; /* ln(E) as computed by hd_math (constant_medium.rs:59) */
   bool motion_uniform = false; /* every moving sphere shares (time0, time1 - time0) */
+  bool media_nested = false;   /* a ConstantMedium inside a Translation/Rotation */
   float motion_t0 = 0, motion_span = 1;
 
   /* ---- device ---- */
@@ -127,5 +128,7 @@ namespace hrt {
 void set_error(const std::string& msg);
 /* implemented in render.hip */
 hrt_status device_upload(hrt_scene* s, int device);
+void flatten_scene(hrt_scene* s);          /* scene.cpp: graph -> layout.h arrays */
+std::vector<uint8_t> build_blob(hrt_scene* s); /* scene.cpp: the arrays in one blob; sets s->off_* */
 void device_release(hrt_scene* s);
 }  // namespace hrt

@@ -87,6 +87,15 @@ class RenderStats(ctypes.Structure):
         [("phase_cycles", ctypes.c_uint64 * 3)]
 
 
+class BlobInfo(ctypes.Structure):
+    """hrt_blob_info (include/hrt/hrt.h)."""
+    _fields_ = [(n, ctypes.c_uint64) for n in ("off_nodes", "off_prims", "off_insts", "off_media", "off_mats", "off_texs",
+                                                "off_perlin", "off_images")] + \
+        [(n, ctypes.c_uint32) for n in ("n_nodes", "main_end", "n_prims", "feature_mask", "cull_mode", "motion_uniform")] + \
+        [("motion_t0", ctypes.c_float), ("motion_span", ctypes.c_float), ("ln_e", ctypes.c_float),
+         ("media_nested", ctypes.c_uint32), ("box_t0", ctypes.c_float), ("box_t1", ctypes.c_float)]
+
+
 class PresetInfo(ctypes.Structure):
     _fields_ = [
         ("look_from", ctypes.c_float * 3),
@@ -117,7 +126,7 @@ EXPORTS = [
     "hrt_node_rotate", "hrt_node_constant_medium", "hrt_node_list", "hrt_node_bvh", "hrt_node_count",
     "hrt_node_bounding_box", "hrt_scene_set_root", "hrt_scene_commit", "hrt_preset_build", "hrt_camera_init",
     "hrt_render_tiles_device", "hrt_render_device", "hrt_render", "hrt_tile_grid", "hrt_scene_get_info",
-    "hrt_debug_device_math", "hrt_debug_trace_path", "hrt_debug_prim_record",
+    "hrt_debug_device_math", "hrt_debug_trace_path", "hrt_debug_scene_blob", "hrt_debug_prim_record",
 ]
 
 _lib = None
@@ -179,6 +188,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hrt_tile_grid": (S, [u32, u32, u32, u32, u32, vp, u32, _U32P]),
         "hrt_scene_get_info": (S, [vp, ctypes.POINTER(SceneInfo)]),
         "hrt_debug_device_math": (S, [i32, vp, vp, vp, u32]),
+        "hrt_debug_scene_blob": (S, [vp, vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(BlobInfo)]),
         "hrt_debug_prim_record": (S, [vp, i32, u32, vp]),
         "hrt_debug_trace_path": (S, [vp, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), u32, u32, u32, u32, vp, _U32P]),
     }
@@ -416,6 +426,16 @@ def trace_path(scene: Scene, cam: Camera, p: RenderParams, x: int, y: int, sampl
         r = out[9 * i:9 * i + 9]
         segs.append((r[0:3].copy(), r[3:6].copy(), float(r[6]), float(r[7]), int(r[8:9].view(np.uint32)[0])))
     return segs, out[9 * max_segments:9 * max_segments + 3].copy()
+
+
+def scene_blob(scene: "Scene"):
+    """The flattened scene (layout.h) as the kernels see it, without a device: (bytes, BlobInfo)."""
+    size = ctypes.c_uint64()
+    info = BlobInfo()
+    _check(load().hrt_debug_scene_blob(scene.h, None, 0, ctypes.byref(size), ctypes.byref(info)))
+    buf = ctypes.create_string_buffer(size.value)
+    _check(load().hrt_debug_scene_blob(scene.h, buf, size.value, ctypes.byref(size), ctypes.byref(info)))
+    return buf, info
 
 
 def prim_record(scene: Scene, index: int, order: int = 0) -> np.ndarray:

@@ -243,6 +243,24 @@ hrt_status hrt_scene_get_info(const hrt_scene* s, hrt_scene_info* info);
 hrt_status hrt_debug_trace_path(hrt_scene* s, const hrt_camera* cam, const hrt_render_params* p, uint32_t x,
                                 uint32_t y, uint32_t sample, uint32_t max_segments, float* out,
                                 uint32_t* n_segments);
+/* The flattened scene as the kernels see it (layout.h sections inside one blob), for host-side
+ * inspection and for tests/native/lane_sim.hip, which runs the kernels' per-lane code on the host.
+ * Flattens the scene if needed (no device involved; the scene stays mutable unless committed).
+ * Call with out == NULL to get the size.  Offsets are byte offsets into the blob. */
+typedef struct hrt_blob_info {
+  uint64_t off_nodes, off_prims, off_insts, off_media, off_mats, off_texs, off_perlin, off_images;
+  uint32_t n_nodes;        /* node-stream entries: main stream + medium boundary subtrees */
+  uint32_t main_end;       /* end of the main stream */
+  uint32_t n_prims;
+  uint32_t feature_mask;
+  uint32_t cull_mode;      /* the default culling (layout.h CULL_*) */
+  uint32_t motion_uniform; /* every moving sphere shares time0 / time1 */
+  float motion_t0, motion_span;
+  float ln_e;
+  uint32_t media_nested;   /* a ConstantMedium inside a Translation/Rotation */
+  float box_t0, box_t1;    /* ray times the BVH boxes are valid for */
+} hrt_blob_info;
+hrt_status hrt_debug_scene_blob(hrt_scene* s, void* out, uint64_t cap, uint64_t* size, hrt_blob_info* info);
 /* The flattened 48-byte record of a primitive (order 0: reference pre-order, 1: SAH streams). */
 hrt_status hrt_debug_prim_record(const hrt_scene* s, int32_t order, uint32_t index, float* out12);
 hrt_status hrt_debug_device_math(int32_t op, const float* x, const float* y, float* out, uint32_t n);

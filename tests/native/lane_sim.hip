@@ -1,0 +1,158 @@
+/*
+ * lane_sim.hip — TEST INFRASTRUCTURE: runs the kernels' per-lane code (hyper-ray-tracer_amd/csrc/lane.h)
+ * on the host, one lane at a time, over the flattened scene of hrt_debug_scene_blob.
+ *
+ * A GPU lane of render_basic_kernel / render_full_kernel executes, for each of its samples, exactly:
+ * start_sample -> { walk to the end with basic_step / full_step; shade } until the path ends, and
+ * sums the samples of a chunk in order (reduce_chunks then adds the chunk sums in chunk order).
+ * Which lanes step together, and when a wave stops to shade, never changes a lane's own sequence of
+ * tests and draws.  So this harness reproduces what the kernels compute per pixel, and
+ * tests/test_lane_sim.py checks it against the CPU oracle (oracle/) without a GPU.  It is built by the
+ * tests (host-only compile) and is not part of libhrt.
+ */
+#include <cstring>
+#include <vector>
+
+#include "lane.h"
+
+using namespace hrt;
+using namespace hrt::lane;
+
+namespace {
+
+/* KIND 0: render_basic_kernel's lane, 1: render_full_kernel's lane, 2: render_kernel's (segment()) */
+template <int CULL, int KIND>
+void render_pixel(const KParams& P, uint32_t px, uint32_t py, float* rgba, uint64_t* cnt) {
+  constexpr bool FULL = KIND == 1;
+  const uint32_t spp = P.spp;
+  const uint32_t chunk = spp <= 32 ? spp : std::max<uint32_t>(32, (spp + 15) / 16); /* render.hip */
+  const uint32_t n_chunks = (spp + chunk - 1) / chunk;
+  const float inf = u2f(0x7f800000u);
+  Counts cn{0u, 0u, 0u, 0u, 0u, 0u};
+  Vec3 total = v3(0.0f, 0.0f, 0.0f);
+  for (uint32_t c = 0; c < n_chunks; c++) {
+    Vec3 sum = v3(0.0f, 0.0f, 0.0f);
+    const uint32_t s_end = std::min(spp, (c + 1) * chunk);
+    for (uint32_t sample = c * chunk; sample < s_end; sample++) {
+      PathState ps;
+      init_path_state(ps);
+      start_sample(P, ps, px, py, sample);
+      if constexpr (KIND == 2) { /* one world.hit per segment() call (render_kernel) */
+        for (;;) {
+          const bool done = segment<CULL, true, true, false>(P, P.nodes, P.prims, ps, cn, nullptr);
+          if (ps.traced) cnt[0]++;
+          if (done) break;
+        }
+        sum = sum + ps.rad;
+        cnt[1]++;
+        continue;
+      }
+      TRay r;
+      set_ray(r, ps.ro, ps.rd, ps.rtime, P);
+      Vec3 wo = ps.ro, wd = ps.rd;
+      for (;;) {
+        bool traced, done;
+        if constexpr (FULL) {
+          FullWalk w{0u, P.main_end, 0u, 0u, P.t_min, inf, G::NONE, inf, 0.0f, G::NONE};
+          if (ps.depth_left == 0) w.i = G::NONE;
+          while (w.i < w.end) full_step<CULL, true>(P, P.nodes, P.prims, w, r, wo, wd, ps.pk, cn);
+          traced = w.i != G::NONE;
+          done = true;
+          if (traced) {
+            ps.pk.segment++;
+            done = shade<true, true>(P, ps, w.wn, w.cl, wo, wd, r.time, r.tau, cn) || ps.depth_left == 0;
+          }
+        } else {
+          uint32_t node = ps.depth_left == 0 ? G::NONE : 0u, winner = G::NONE;
+          float closest = inf;
+          while (node < P.main_end) basic_step<CULL, true>(P, P.nodes, P.prims, node, r, closest, winner, cn);
+          traced = node != G::NONE;
+          done = !traced ||
+                 shade<false, true>(P, ps, winner, closest, r.o, r.d, r.time, r.tau, cn) || ps.depth_left == 0;
+        }
+        if (traced) cnt[0]++;
+        if (done) break;
+        set_dir(r, ps.ro, ps.rd); /* the scattered ray keeps the sample's shutter time */
+        wo = ps.ro;
+        wd = ps.rd;
+      }
+      sum = sum + ps.rad;
+      cnt[1]++;
+    }
+    total = c == 0 ? sum : total + sum;
+  }
+  const float scale = 1.0f / (float)spp;
+  rgba[0] = sqrtf(total.x * scale);
+  rgba[1] = sqrtf(total.y * scale);
+  rgba[2] = sqrtf(total.z * scale);
+  rgba[3] = 1.0f;
+  cnt[2] += cn.nodes;
+  cnt[3] += cn.prims;
+  cnt[4] += cn.tex;
+}
+
+}  // namespace
+
+extern "C" {
+
+/* kernel: 0 = render_basic_kernel's lane, 1 = render_full_kernel's, 2 = render_kernel's (segment
+ * at a time); cull: layout.h CULL_*.
+ * cnt[0..4] += segments, samples, node visits, primitive tests, texture evaluations. */
+int lane_sim_render(const void* blob, const hrt_blob_info* bi, const hrt_camera* cam, const hrt_render_params* p,
+                    int kernel, int cull, uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, float* rgba,
+                    uint64_t* cnt) {
+  const uint8_t* base = (const uint8_t*)blob;
+  KParams P;
+  memset(&P, 0, sizeof(P));
+  P.nodes = (const G::Node*)(base + bi->off_nodes);
+  P.prims = (const G::Prim*)(base + bi->off_prims);
+  P.insts = (const G::Inst*)(base + bi->off_insts);
+  P.media = (const G::Medium*)(base + bi->off_media);
+  P.mats = (const G::Mat*)(base + bi->off_mats);
+  P.texs = (const G::Tex*)(base + bi->off_texs);
+  P.perlin = (const G::Perlin*)(base + bi->off_perlin);
+  P.images = base + bi->off_images;
+  P.main_end = bi->main_end;
+  P.ln_e = bi->ln_e;
+  P.motion_uniform = bi->motion_uniform;
+  P.motion_t0 = bi->motion_t0;
+  P.motion_span = bi->motion_span;
+  P.cam_origin = v3(cam->origin[0], cam->origin[1], cam->origin[2]);
+  P.cam_llc = v3(cam->lower_left_corner[0], cam->lower_left_corner[1], cam->lower_left_corner[2]);
+  P.cam_h = v3(cam->horizontal[0], cam->horizontal[1], cam->horizontal[2]);
+  P.cam_v = v3(cam->vertical[0], cam->vertical[1], cam->vertical[2]);
+  P.cam_u = v3(cam->u[0], cam->u[1], cam->u[2]);
+  P.cam_vv = v3(cam->v[0], cam->v[1], cam->v[2]);
+  P.lens_radius = cam->lens_radius;
+  P.time0 = cam->time0;
+  P.time1 = cam->time1;
+  P.W = p->width;
+  P.H = p->height;
+  P.spp = p->samples;
+  P.max_depth = p->max_depth;
+  P.sample_offset = p->sample_offset;
+  P.t_min = p->t_min;
+  P.background = v3(p->background[0], p->background[1], p->background[2]);
+  P.seed = p->seed;
+  if (kernel == 0 && (bi->feature_mask & ~G::F_BASIC) != 0) return 1; /* not a sphere scene */
+  for (uint32_t y = 0; y < h; y++)
+    for (uint32_t x = 0; x < w; x++) {
+      float* o = rgba + 4 * ((size_t)y * w + x);
+      if (kernel == 0) {
+        if (cull == G::CULL_EXACT) render_pixel<G::CULL_EXACT, 0>(P, x0 + x, y0 + y, o, cnt);
+        else if (cull == G::CULL_SLAB) render_pixel<G::CULL_SLAB, 0>(P, x0 + x, y0 + y, o, cnt);
+        else render_pixel<G::CULL_REFERENCE, 0>(P, x0 + x, y0 + y, o, cnt);
+      } else if (kernel == 1) {
+        if (cull == G::CULL_EXACT) render_pixel<G::CULL_EXACT, 1>(P, x0 + x, y0 + y, o, cnt);
+        else if (cull == G::CULL_SLAB) render_pixel<G::CULL_SLAB, 1>(P, x0 + x, y0 + y, o, cnt);
+        else render_pixel<G::CULL_REFERENCE, 1>(P, x0 + x, y0 + y, o, cnt);
+      } else {
+        if (cull == G::CULL_EXACT) render_pixel<G::CULL_EXACT, 2>(P, x0 + x, y0 + y, o, cnt);
+        else if (cull == G::CULL_SLAB) render_pixel<G::CULL_SLAB, 2>(P, x0 + x, y0 + y, o, cnt);
+        else render_pixel<G::CULL_REFERENCE, 2>(P, x0 + x, y0 + y, o, cnt);
+      }
+    }
+  return 0;
+}
+
+}  // extern "C"
