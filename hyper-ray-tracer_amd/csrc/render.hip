@@ -630,8 +630,12 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
                     : (s->g_nodes.size() * sizeof(G::Node) + s->g_prims.size() * sizeof(G::Prim));
   pl.lds = (flags & HRT_RENDER_NO_LDS) == 0 && pl.smem <= (pl.fast ? LDS_FAST_MAX : LDS_SCENE_MAX);
   const char* k = getenv("HRT_KERNEL");
-  /* the segment-at-a-time kernel: media inside instances (not in any reference scene), diagnostics */
-  pl.general = (k && strcmp(k, "general") == 0) || s->media_nested;
+  /* General scenes run the segment-at-a-time kernel by default; render_full_kernel (persistent walks)
+   * is opt-in (HRT_KERNEL=persistent) until it has been measured and validated on the GPU.  Sphere
+   * scenes can be sent to the segment kernel for diagnostics (HRT_KERNEL=general). */
+  const bool persistent = k && strcmp(k, "persistent") == 0;
+  pl.general = (k && strcmp(k, "general") == 0) || s->media_nested || (pl.full && !persistent);
+  if (pl.general && pl.full) pl.lds = false; /* render_kernel<FULL> reads the scene from global memory */
   return pl;
 }
 

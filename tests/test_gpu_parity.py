@@ -188,3 +188,28 @@ def test_headline_frame_exact_equals_reference_traversal(earth):
     assert np.isfinite(ex).all() and (ex[..., 3] == 1).all()
     again = hrt.render(s, cam, hrt.params(W, H, 500, 50, 1, bg))
     assert np.array_equal(again, ex)
+
+
+def _has_gpu():
+    import torch
+
+    return torch.cuda.is_available()
+
+
+@pytest.mark.gpu_wip
+@pytest.mark.skipif(not _has_gpu(), reason="needs a GPU")
+@pytest.mark.parametrize("name,w,h,spp", [("cornell", 40, 40, 16), ("cornell_smoke", 40, 40, 16), ("final", 40, 40, 8),
+                                          ("features", 64, 36, 16), ("earth_perlin", 48, 27, 16), ("simple_light", 48, 27, 16)])
+def test_persistent_general_kernel_equals_segment_kernel(earth, monkeypatch, name, w, h, spp):
+    """render_full_kernel (HRT_KERNEL=persistent) against the default segment-at-a-time kernel: the
+    per-lane code is shared (csrc/lane.h, host-checked by tests/test_lane_sim.py), so the images must be
+    identical bit for bit."""
+    s = hrt.preset(name, 1, earth)
+    s.commit()
+    cam = hrt.preset_camera(s.info, w, h)
+    p = hrt.params(w, h, spp, 50, 7, tuple(s.info.background))
+    a, sa = hrt.render(s, cam, p, stats=True)
+    monkeypatch.setenv("HRT_KERNEL", "persistent")
+    b, sb = hrt.render(s, cam, p, stats=True)
+    assert sa.segments == sb.segments
+    assert np.array_equal(a, b)
