@@ -126,7 +126,7 @@ EXPORTS = [
     "hrt_node_rotate", "hrt_node_constant_medium", "hrt_node_list", "hrt_node_bvh", "hrt_node_count",
     "hrt_node_bounding_box", "hrt_scene_set_root", "hrt_scene_commit", "hrt_preset_build", "hrt_camera_init",
     "hrt_render_tiles_device", "hrt_render_device", "hrt_render", "hrt_tile_grid", "hrt_scene_get_info",
-    "hrt_debug_device_math", "hrt_debug_trace_path", "hrt_debug_scene_blob", "hrt_debug_prim_record",
+    "hrt_debug_device_math", "hrt_debug_trace_path", "hrt_debug_scene_blob", "hrt_image_write", "hrt_debug_prim_record",
 ]
 
 _lib = None
@@ -190,6 +190,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hrt_debug_device_math": (S, [i32, vp, vp, vp, u32]),
         "hrt_debug_scene_blob": (S, [vp, vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(BlobInfo)]),
         "hrt_debug_prim_record": (S, [vp, i32, u32, vp]),
+        "hrt_image_write": (S, [ctypes.c_char_p, vp, u32, u32, i32]),
         "hrt_debug_trace_path": (S, [vp, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), u32, u32, u32, u32, vp, _U32P]),
     }
     for name, (res, args) in sig.items():
@@ -426,6 +427,30 @@ def trace_path(scene: Scene, cam: Camera, p: RenderParams, x: int, y: int, sampl
         r = out[9 * i:9 * i + 9]
         segs.append((r[0:3].copy(), r[3:6].copy(), float(r[6]), float(r[7]), int(r[8:9].view(np.uint32)[0])))
     return segs, out[9 * max_segments:9 * max_segments + 3].copy()
+
+
+IMAGE_PFM, IMAGE_PPM = 0, 1
+
+
+def write_image(path: str, rgba: np.ndarray, fmt: Optional[int] = None) -> None:
+    """Write a render result ((h, w, 4) f32, row 0 = bottom) as PFM (exact floats) or 8-bit PPM;
+    the format follows the extension unless given."""
+    img = np.ascontiguousarray(rgba, np.float32)
+    if img.ndim != 3 or img.shape[2] != 4:
+        raise ValueError("expected an (h, w, 4) float32 frame")
+    if fmt is None:
+        fmt = IMAGE_PPM if str(path).lower().endswith(".ppm") else IMAGE_PFM
+    _check(load().hrt_image_write(str(path).encode(), img.ctypes.data, img.shape[1], img.shape[0], fmt))
+
+
+def read_pfm(path: str) -> np.ndarray:
+    """Read a PFM written by write_image back into an (h, w, 3) float32 array (row 0 = bottom)."""
+    with open(path, "rb") as f:
+        assert f.readline().strip() == b"PF"
+        w, h = (int(v) for v in f.readline().split())
+        scale = float(f.readline())
+        data = np.frombuffer(f.read(), "<f4" if scale < 0 else ">f4")
+    return data.reshape(h, w, 3).astype(np.float32)
 
 
 def scene_blob(scene: "Scene"):

@@ -89,6 +89,12 @@ enum {
                                     (traversal order changes which of two near-equal f32 hits wins) */
 };
 
+/* hrt_image_write formats (the reference only displays its frame) */
+enum {
+  HRT_IMAGE_PFM = 0, /* float RGB, little-endian, rows bottom to top: the frame bit for bit */
+  HRT_IMAGE_PPM = 1  /* 8-bit binary RGB, rows top to bottom, 256 * clamp(c, 0, 0.999) per channel */
+};
+
 typedef struct hrt_tile {
   uint32_t x, y, w, h; /* image coordinates, y up */
 } hrt_tile;
@@ -237,6 +243,9 @@ typedef struct hrt_scene_info {
 hrt_status hrt_scene_get_info(const hrt_scene* s, hrt_scene_info* info);
 /* Evaluate the shared deterministic math on the DEVICE (op: 0 sin,1 cos,2 acos,3 atan2,4 ln,
  * 5 pow5, 6 tan) for n inputs; used by the GPU KAT test to prove host/device bit identity. */
+/* Write an RGBA f32 frame (w x h, row-major, row 0 = image y 0 = bottom, as the render calls produce;
+ * alpha is dropped) to `path` in an HRT_IMAGE_* format. */
+hrt_status hrt_image_write(const char* path, const float* rgba, uint32_t w, uint32_t h, int32_t format);
 /* Trace ONE path (pixel x,y of the full image; sample index) on the device with the traversal the
  * renderer would use for these params; out[9*i .. 9*i+8] = origin, direction, time, closest t,
  * winner id (bits) of segment i; out[9*max_segments .. +2] = the path's radiance. */
