@@ -47,12 +47,25 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--save", default="", help="write rank 0's last timed frame here (.pfm exact / .ppm 8-bit)")
     return ap.parse_args()
+
+
+def host_cpu():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def cpu_baseline(args, rank_segments_per_sample):
     """The CPU restatement of the reference path (oracle/, 'port'), 80x80 tiles on a thread pool,
-    timed on this host on a bounded band of the same frame (rows through the middle of the image)."""
+    timed on this host on a bounded band of the same frame (rows through the middle of the image),
+    plus a one-thread rate on a short band."""
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
 
@@ -69,14 +82,24 @@ def cpu_baseline(args, rank_segments_per_sample):
     t0 = time.perf_counter()
     _, c = o.render(W, H, args.spp, args.depth, seed=args.seed, region=(0, y0, W, rows), threads=threads)
     dt = time.perf_counter() - t0
+    # one thread, a short stretch of the middle row (~2 s)
+    px1 = max(8, min(W, int(2.0 * rate / threads / max(1.0, seg_per_row / W))))
+    t1 = time.perf_counter()
+    _, c1 = o.render(W, H, args.spp, args.depth, seed=args.seed, region=(0, H // 2, px1, 1), threads=1)
+    dt1 = time.perf_counter() - t1
     return {
         "value": round(c["segments"] / dt / 1e6, 4),
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
+        "label": "CPU restatement of the reference path (oracle/, not the reference binary)",
         "sample": f"rows {y0}..{y0 + rows - 1} of the {W}x{H} frame at {args.spp} spp "
                   f"({c['samples']} samples, {c['segments']} rays, {dt:.1f} s); reference aabb.rs culling",
         "segments_per_sample": round(c["segments"] / c["samples"], 4),
+        "one_core_value": round(c1["segments"] / dt1 / 1e6, 4),
+        "one_core_sample": f"{px1} pixels of row {H // 2} at {args.spp} spp ({c1['segments']} rays, {dt1:.1f} s)",
+        "host_cpu": host_cpu(),
+        "nproc": os.cpu_count(),
     }
 
 
@@ -176,6 +199,12 @@ def main():
                     roofline["traffic_source"] = pm[key]["source"]
             except (OSError, ValueError, KeyError):
                 pass
+
+    if rank == 0 and args.save:
+        if tiles == [(0, 0, W, H)]:
+            hrt.write_image(args.save, out.view(H, W, 4).cpu().numpy())
+        else:
+            print("--save: rank 0 holds a tile set, not the frame; nothing written", file=sys.stderr)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
