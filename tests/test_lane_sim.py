@@ -43,11 +43,11 @@ def sim(tmp_path_factory):
     return L
 
 
-def sim_render(L, name, w, h, spp, depth, seed, earth, kernel, cull, region=None):
+def sim_render(L, name, w, h, spp, depth, seed, earth, kernel, cull, region=None, sample_offset=0, t_min=0.001):
     s = hrt.preset(name, 1, earth)
     blob, info = hrt.scene_blob(s)
     cam = hrt.preset_camera(s.info, w, h)
-    p = hrt.params(w, h, spp, depth, seed, tuple(s.info.background))
+    p = hrt.params(w, h, spp, depth, seed, tuple(s.info.background), sample_offset=sample_offset, t_min=t_min)
     x0, y0, rw, rh = region if region is not None else (0, 0, w, h)
     out = np.zeros((rh, rw, 4), np.float32)
     cnt = np.zeros(8, np.uint64)
@@ -57,8 +57,9 @@ def sim_render(L, name, w, h, spp, depth, seed, earth, kernel, cull, region=None
     return out, {"segments": int(cnt[0]), "samples": int(cnt[1]), "nodes": int(cnt[2]), "prims": int(cnt[3])}
 
 
-def oracle_render(name, w, h, spp, depth, seed, earth, region=None):
-    return O.OracleScene(hrt.PRESETS[name], 1, earth).render(w, h, spp, depth, seed=seed, region=region, threads=8)
+def oracle_render(name, w, h, spp, depth, seed, earth, region=None, sample_offset=0, t_min=0.001):
+    return O.OracleScene(hrt.PRESETS[name], 1, earth).render(w, h, spp, depth, seed=seed, region=region, threads=8,
+                                                             sample_offset=sample_offset, t_min=t_min)
 
 
 CASES = [
@@ -122,3 +123,35 @@ def test_region_of_frame(sim, earth):
     full, _ = sim_render(sim, "final", 32, 32, 2, 50, 9, earth, kernel=1, cull=CULL_EXACT)
     part, _ = sim_render(sim, "final", 32, 32, 2, 50, 9, earth, kernel=1, cull=CULL_EXACT, region=(5, 7, 11, 9))
     assert np.array_equal(part, full[7:16, 5:16])
+
+
+@pytest.mark.parametrize("kernel,name", [(0, "random"), (1, "cornell_smoke"), (1, "features")])
+def test_sample_offset_and_t_min(sim, earth, kernel, name):
+    """bench.py --scaling weak gives rank r the samples [r*spp, (r+1)*spp) (sample_offset); t_min is
+    application.rs:482's 0.001 by default and a render parameter here."""
+    for off, tmin in ((500, 0.001), (0, 0.01), (7, 0.0)):
+        img, st = sim_render(sim, name, 32, 18, 4, 50, 11, earth, kernel=kernel, cull=CULL_EXACT,
+                             sample_offset=off, t_min=tmin)
+        ref, cnt = oracle_render(name, 32, 18, 4, 50, 11, earth, sample_offset=off, t_min=tmin)
+        assert st["segments"] == cnt["segments"], (off, tmin)
+        assert np.abs(img - ref).max() <= TOL
+
+
+@pytest.mark.parametrize("depth", [1, 2, 3])
+def test_depth_caps(sim, earth, depth):
+    for kernel, name in ((0, "random"), (1, "final")):
+        img, st = sim_render(sim, name, 24, 16, 4, depth, 2, earth, kernel=kernel, cull=CULL_EXACT)
+        ref, cnt = oracle_render(name, 24, 16, 4, depth, 2, earth)
+        assert st["segments"] == cnt["segments"]
+        assert np.abs(img - ref).max() <= TOL
+
+
+def test_headline_frame_band_at_500_spp(sim, earth):
+    """Two rows through the middle of the BASELINE frame (1920x1080, 500 spp, depth 50: 16 sample
+    chunks) on the sphere kernel's lane, against the oracle."""
+    region = (0, 539, 1920, 2)
+    img, st = sim_render(sim, "random", 1920, 1080, 500, 50, 1, earth, kernel=0, cull=CULL_EXACT, region=region)
+    ref, cnt = oracle_render("random", 1920, 1080, 500, 50, 1, earth, region=region)
+    assert st["samples"] == 1920 * 2 * 500
+    assert st["segments"] == cnt["segments"]
+    assert np.abs(img - ref).max() <= TOL
