@@ -563,7 +563,8 @@ HRT_LANE_NI Vec3 tex_heavy(const KParams& P, const G::Tex& T, float u, float v, 
         float scale = T.a[0];
         Vec3 q = scale * p;
         float accumulator = 0.0f, weight = 1.0f;
-        for (int o = 0; o < 7; o++) {
+#pragma unroll 1
+        for (int o = 0; o < 7; o++) { /* rolled: keeps the callee (and so its callers) small */
           accumulator += weight * perlin_noise(pn, q);
           weight *= 0.5f;
           q = q * 2.0f;
