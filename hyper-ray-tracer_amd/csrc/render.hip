@@ -918,6 +918,94 @@ hrt_status hrt_render(hrt_scene* s, const hrt_camera* cam, const hrt_render_para
   return st;
 }
 
+/* Application::render with progressive tile delivery (application.rs:393-475, the Tile messages of
+ * :45-52 / :461-472): the rank's share of the tile grid is rendered in launches of `batch` tiles on a
+ * stream of its own; while batch k+1 renders, batch k (copied to pinned memory) is handed to `fn` tile
+ * by tile in grid order.  With `stats` each batch's counters are read as it completes (the host then
+ * waits for every launch before consuming the previous batch). */
+hrt_status hrt_render_progressive(hrt_scene* s, const hrt_camera* cam, const hrt_render_params* p,
+                                  uint32_t tile_size, uint32_t rank, uint32_t world, uint32_t batch,
+                                  hrt_tile_fn fn, void* user, hrt_render_stats* stats) {
+  if (!s || !cam || !p || !fn || tile_size == 0 || batch == 0 || world == 0 || rank >= world) {
+    set_error("hrt_render_progressive: bad argument");
+    return HRT_ERR_INVALID_ARG;
+  }
+  if (!s->committed) {
+    set_error("scene not committed");
+    return HRT_ERR_STATE;
+  }
+  uint32_t n = 0;
+  hrt_status st = hrt_tile_grid(p->width, p->height, tile_size, rank, world, nullptr, 0, &n);
+  if (st != HRT_OK) return st;
+  std::vector<hrt_tile> tiles(n);
+  st = hrt_tile_grid(p->width, p->height, tile_size, rank, world, tiles.data(), n, &n);
+  if (st != HRT_OK) return st;
+  if (stats) memset(stats, 0, sizeof(*stats));
+  const size_t slot_floats = (size_t)batch * tile_size * tile_size * 4;
+  float* d_buf[2] = {nullptr, nullptr};
+  float* h_buf[2] = {nullptr, nullptr};
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  st = hguard([&] {
+    DeviceGuard dg(s->device);
+    hip_check(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
+    for (int k = 0; k < 2; k++) {
+      hip_check(hipMalloc((void**)&d_buf[k], slot_floats * sizeof(float)), "hipMalloc(progressive)");
+      hip_check(hipHostMalloc((void**)&h_buf[k], slot_floats * sizeof(float), hipHostMallocDefault),
+                "hipHostMalloc(progressive)");
+      hip_check(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming), "hipEventCreate");
+    }
+    const uint32_t n_batches = (n + batch - 1) / batch;
+    for (uint32_t b = 0; b <= n_batches; b++) {
+      if (b < n_batches) { /* render batch b into slot b % 2, copy it back, mark it */
+        const uint32_t first = b * batch, cnt = std::min(batch, n - first);
+        hrt_render_stats bs;
+        const hrt_status r = hrt_render_tiles_device(s, cam, p, tiles.data() + first, cnt, d_buf[b % 2], stream,
+                                                     stats ? &bs : nullptr);
+        if (r != HRT_OK) throw HipError{r, hrt_last_error()};
+        size_t px = 0;
+        for (uint32_t t = 0; t < cnt; t++) px += (size_t)tiles[first + t].w * tiles[first + t].h;
+        hip_check(hipMemcpyAsync(h_buf[b % 2], d_buf[b % 2], px * 16, hipMemcpyDeviceToHost, stream),
+                  "hipMemcpyAsync(progressive)");
+        hip_check(hipEventRecord(ev[b % 2], stream), "hipEventRecord(progressive)");
+        if (stats) {
+          stats->segments += bs.segments;
+          stats->samples += bs.samples;
+          stats->pixels += bs.pixels;
+          stats->node_visits += bs.node_visits;
+          stats->prim_tests += bs.prim_tests;
+          stats->tex_evals += bs.tex_evals;
+        }
+      }
+      if (b >= 1) { /* hand batch b-1 over, tile by tile */
+        const uint32_t k = b - 1, first = k * batch, cnt = std::min(batch, n - first);
+        hip_check(hipEventSynchronize(ev[k % 2]), "hipEventSynchronize(progressive)");
+        size_t off = 0;
+        for (uint32_t t = 0; t < cnt; t++) {
+          const hrt_tile& tl = tiles[first + t];
+          hrt_tile_pixels tp{tl.x / tile_size, tl.y / tile_size, tl.w, tl.h, h_buf[k % 2] + off * 4};
+          fn(&tp, user);
+          off += (size_t)tl.w * tl.h;
+        }
+      }
+    }
+  });
+  {
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(s->device);
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (int k = 0; k < 2; k++) {
+      if (ev[k]) (void)hipEventDestroy(ev[k]);
+      if (d_buf[k]) (void)hipFree(d_buf[k]);
+      if (h_buf[k]) (void)hipHostFree(h_buf[k]);
+    }
+    if (stream) (void)hipStreamDestroy(stream);
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  return st;
+}
+
 hrt_status hrt_debug_trace_path(hrt_scene* s, const hrt_camera* cam, const hrt_render_params* p, uint32_t x,
                                 uint32_t y, uint32_t sample, uint32_t max_segments, float* out, uint32_t* n_segments) {
   return hguard([&] {

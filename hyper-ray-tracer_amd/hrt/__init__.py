@@ -87,6 +87,15 @@ class RenderStats(ctypes.Structure):
         [("phase_cycles", ctypes.c_uint64 * 3)]
 
 
+class TilePixels(ctypes.Structure):
+    """hrt_tile_pixels (include/hrt/hrt.h)."""
+    _fields_ = [("x", ctypes.c_uint32), ("y", ctypes.c_uint32), ("width", ctypes.c_uint32),
+                ("height", ctypes.c_uint32), ("pixels", ctypes.POINTER(ctypes.c_float))]
+
+
+TILE_FN = ctypes.CFUNCTYPE(None, ctypes.POINTER(TilePixels), ctypes.c_void_p)
+
+
 class BlobInfo(ctypes.Structure):
     """hrt_blob_info (include/hrt/hrt.h)."""
     _fields_ = [(n, ctypes.c_uint64) for n in ("off_nodes", "off_prims", "off_insts", "off_media", "off_mats", "off_texs",
@@ -126,7 +135,7 @@ EXPORTS = [
     "hrt_node_rotate", "hrt_node_constant_medium", "hrt_node_list", "hrt_node_bvh", "hrt_node_count",
     "hrt_node_bounding_box", "hrt_scene_set_root", "hrt_scene_commit", "hrt_preset_build", "hrt_camera_init",
     "hrt_render_tiles_device", "hrt_render_device", "hrt_render", "hrt_tile_grid", "hrt_scene_get_info",
-    "hrt_debug_device_math", "hrt_debug_trace_path", "hrt_debug_scene_blob", "hrt_image_write", "hrt_debug_prim_record",
+    "hrt_debug_device_math", "hrt_debug_trace_path", "hrt_debug_scene_blob", "hrt_image_write", "hrt_render_progressive", "hrt_debug_prim_record",
 ]
 
 _lib = None
@@ -191,6 +200,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hrt_debug_scene_blob": (S, [vp, vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(BlobInfo)]),
         "hrt_debug_prim_record": (S, [vp, i32, u32, vp]),
         "hrt_image_write": (S, [ctypes.c_char_p, vp, u32, u32, i32]),
+        "hrt_render_progressive": (S, [vp, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), u32, u32, u32, u32,
+                                       TILE_FN, vp, ctypes.POINTER(RenderStats)]),
         "hrt_debug_trace_path": (S, [vp, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), u32, u32, u32, u32, vp, _U32P]),
     }
     for name, (res, args) in sig.items():
@@ -451,6 +462,37 @@ def read_pfm(path: str) -> np.ndarray:
         scale = float(f.readline())
         data = np.frombuffer(f.read(), "<f4" if scale < 0 else ">f4")
     return data.reshape(h, w, 3).astype(np.float32)
+
+
+class TileMessage:
+    """application.rs:45-52 Tile (the mpsc message): tile-grid position, size, and (height, width, 4)
+    RGBA pixels (row 0 = bottom)."""
+
+    def __init__(self, x, y, width, height, pixels):
+        self.x, self.y, self.width, self.height, self.pixels = x, y, width, height, pixels
+
+
+def render_progressive(scene: "Scene", cam: Camera, p: RenderParams, on_tile, tile_size: int = 80, rank: int = 0,
+                       world: int = 1, batch: int = 64, stats: bool = False):
+    """Application::render with progressive delivery: on_tile(TileMessage) is called for every tile of this
+    rank's share of the grid, batch by batch, while the next batch renders (hrt_render_progressive)."""
+    err = []
+
+    def cb(tp, _user):
+        try:
+            t = tp.contents
+            px = np.ctypeslib.as_array(t.pixels, shape=(t.height * t.width * 4,)).reshape(t.height, t.width, 4).copy()
+            on_tile(TileMessage(t.x, t.y, t.width, t.height, px))
+        except BaseException as e:  # noqa: BLE001 - re-raised after the C call returns
+            err.append(e)
+
+    fn = TILE_FN(cb)
+    st = RenderStats()
+    _check(load().hrt_render_progressive(scene.h, ctypes.byref(cam), ctypes.byref(p), tile_size, rank, world, batch,
+                                         fn, None, ctypes.byref(st) if stats else None))
+    if err:
+        raise err[0]
+    return st if stats else None
 
 
 def scene_blob(scene: "Scene"):

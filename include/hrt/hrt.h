@@ -217,6 +217,22 @@ hrt_status hrt_camera_init(hrt_camera* cam, const float look_from[3], const floa
 hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hrt_render_params* p,
                                    const hrt_tile* tiles, uint32_t n_tiles, float* d_rgba,
                                    void* stream, hrt_render_stats* stats);
+/* One delivered tile (application.rs:45-52 Tile): tile-grid indices (pixel origin = index * tile_size),
+ * size in pixels, and RGBA f32 pixels row-major in the tile (row 0 = bottom).  `pixels` is valid only
+ * during the callback. */
+typedef struct hrt_tile_pixels {
+  uint32_t x, y;
+  uint32_t width, height;
+  const float* pixels;
+} hrt_tile_pixels;
+typedef void (*hrt_tile_fn)(const hrt_tile_pixels* tile, void* user);
+/* Application::render with progressive delivery (application.rs:393-475 + the mpsc receive of
+ * :284-306): this rank's tiles of the hrt_tile_grid(width, height, tile_size, rank, world) grid are
+ * rendered in launches of `batch` tiles; each finished batch is copied back and passed to `fn` tile by
+ * tile (grid order) while the next batch renders.  Pixels are those of hrt_render on the same tile. */
+hrt_status hrt_render_progressive(hrt_scene* s, const hrt_camera* cam, const hrt_render_params* p,
+                                  uint32_t tile_size, uint32_t rank, uint32_t world, uint32_t batch,
+                                  hrt_tile_fn fn, void* user, hrt_render_stats* stats);
 /* One region into device memory. */
 hrt_status hrt_render_device(hrt_scene* s, const hrt_camera* cam, const hrt_render_params* p,
                              uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, float* d_rgba,

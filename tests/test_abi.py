@@ -182,3 +182,16 @@ def test_commit_without_a_device_fails_loudly():
     with pytest.raises(hrt.HrtError) as e:
         s.commit(0)
     assert e.value.status == hrt.ERR_HIP
+
+
+def test_progressive_render_argument_errors():
+    s = hrt.preset("two_spheres", 1)
+    cam = hrt.preset_camera(s.info, 16, 16)
+    p = hrt.params(16, 16, 1)
+    with pytest.raises(hrt.HrtError) as e:       # not committed
+        hrt.render_progressive(s, cam, p, lambda t: None, tile_size=8)
+    assert e.value.status == hrt.ERR_STATE
+    for kw in ({"tile_size": 0}, {"batch": 0}, {"rank": 2, "world": 2}):
+        with pytest.raises(hrt.HrtError) as e:
+            hrt.render_progressive(s, cam, p, lambda t: None, **{"tile_size": 8, **kw})
+        assert e.value.status == hrt.ERR_INVALID_ARG

@@ -213,3 +213,29 @@ def test_persistent_general_kernel_equals_segment_kernel(earth, monkeypatch, nam
     b, sb = hrt.render(s, cam, p, stats=True)
     assert sa.segments == sb.segments
     assert np.array_equal(a, b)
+
+
+@pytest.mark.gpu_wip
+@pytest.mark.skipif(not _has_gpu(), reason="needs a GPU")
+@pytest.mark.parametrize("batch,world", [(1, 1), (5, 1), (64, 1), (3, 2)])
+def test_progressive_tiles_assemble_the_frame(earth, batch, world):
+    """hrt_render_progressive: every tile of the grid arrives once, in grid order, with
+    the pixels hrt_render gives for the whole frame."""
+    W, H, T = 200, 130, 40
+    s = hrt.preset("random", 1, earth)
+    s.commit()
+    cam = hrt.preset_camera(s.info, W, H)
+    p = hrt.params(W, H, 8, 50, 3, tuple(s.info.background))
+    full = hrt.render(s, cam, p)
+    frame = np.full((H, W, 4), np.nan, np.float32)
+    seen = []
+    for rank in range(world):
+        def on_tile(t):
+            seen.append((t.x, t.y))
+            x0, y0 = t.x * T, t.y * T
+            assert np.isnan(frame[y0:y0 + t.height, x0:x0 + t.width]).all()
+            frame[y0:y0 + t.height, x0:x0 + t.width] = t.pixels
+        st = hrt.render_progressive(s, cam, p, on_tile, tile_size=T, rank=rank, world=world, batch=batch, stats=True)
+        assert st.samples == sum(t[2] * t[3] for t in hrt.tile_grid(W, H, T, rank, world)) * 8
+    assert len(seen) == len(set(seen)) == len(hrt.tile_grid(W, H, T))
+    assert np.array_equal(frame, full)
