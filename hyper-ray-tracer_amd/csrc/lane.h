@@ -28,6 +28,10 @@ namespace G = hrt::gpu;
 
 HRT_LANE_FI uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
 
+#ifndef HRT_EXP_PK
+#define HRT_EXP_PK 0 /* experiment: packed-f32 box test (A/B on the GPU before it becomes the default) */
+#endif
+
 /* ------------------------------------------------------------------ kernel parameters */
 struct KParams {
   const G::Node* nodes;
@@ -128,21 +132,35 @@ HRT_LANE_FI float4 ld4(const void* p) { return *reinterpret_cast<const float4*>(
 template <int CULL>
 HRT_LANE_FI bool box_hit(const float4& a, const float4& b, const TRay& r, float tmin,
                                         float tmax, bool ref_only = false) {
+  const float inv[3] = {r.inv.x, r.inv.y, r.inv.z};
+  float dmn[3], dmx[3], t0[3], t1[3];
+#if HRT_EXP_PK
+  /* x and y in packed f32 (v_pk_add_f32 / v_pk_mul_f32: the same IEEE operations, two per issue) */
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 oxy = {r.o.x, r.o.y}, ixy = {r.inv.x, r.inv.y};
+  const f2 dmnxy = f2{a.x, a.y} - oxy, dmxxy = f2{b.x, b.y} - oxy;
+  const f2 t0xy = dmnxy * ixy, t1xy = dmxxy * ixy;
+  dmn[0] = dmnxy.x; dmn[1] = dmnxy.y; dmn[2] = a.z - r.o.z;
+  dmx[0] = dmxxy.x; dmx[1] = dmxxy.y; dmx[2] = b.z - r.o.z;
+  t0[0] = t0xy.x; t0[1] = t0xy.y; t0[2] = dmn[2] * inv[2];
+  t1[0] = t1xy.x; t1[1] = t1xy.y; t1[2] = dmx[2] * inv[2];
+#else
   const float mn[3] = {a.x, a.y, a.z}, mx[3] = {b.x, b.y, b.z};
-  const float o[3] = {r.o.x, r.o.y, r.o.z}, inv[3] = {r.inv.x, r.inv.y, r.inv.z};
-  float dmn[3], dmx[3];
+  const float o[3] = {r.o.x, r.o.y, r.o.z};
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     dmn[k] = mn[k] - o[k];
     dmx[k] = mx[k] - o[k];
+    t0[k] = dmn[k] * inv[k];
+    t1[k] = dmx[k] * inv[k];
   }
+#endif
   float ts[3], te[3];
 #pragma unroll
   for (int k = 0; k < 3; k++) {
-    const float t0 = dmn[k] * inv[k], t1 = dmx[k] * inv[k];
     const bool neg = inv[k] < 0.0f; /* aabb.rs:28-29 swap */
-    ts[k] = neg ? t1 : t0;
-    te[k] = neg ? t0 : t1;
+    ts[k] = neg ? t1[k] : t0[k];
+    te[k] = neg ? t0[k] : t1[k];
   }
   if (CULL == G::CULL_SLAB) {
     const float lo = fmaxf(fmaxf(fmaxf(ts[0], tmin), ts[1]), ts[2]);
