@@ -65,6 +65,7 @@ struct KParams {
   uint32_t n_nodes;    /* node-stream entries to stage in LDS */
   uint32_t stream_len; /* FAST: length of one octant stream */
   uint32_t postpone;   /* BASIC kernel: lanes that must have finished their walk before a wave shades */
+  uint32_t prim_batch; /* BASIC kernel: lanes that must wait for a primitive test before the wave runs them */
   uint32_t walk_cap;   /* watchdog: more consecutive walk-loop iterations than any valid walk needs */
   uint32_t motion_uniform; /* every moving sphere has time0 = motion_t0, time1 - time0 = motion_span */
   float motion_t0, motion_span;
@@ -82,7 +83,7 @@ struct TRay {
   Vec3 o, d, inv;
   float time;
   float dd;  /* dot(d, d): sphere.rs:42 `a`, constant for the ray */
-  float rdd; /* RN(1 / dd), for div_dd */
+  float rdd; /* RN(1 / dd) for div_rn, or NaN when dd is outside div_rn's fast domain */
   float tau; /* (time - time0) / (time1 - time0) of the scene's moving spheres (uniform motion only) */
 };
 
@@ -91,14 +92,29 @@ struct TRay {
  * residual x - q0*a is exact in an fma, and RN(q0 + residual*y) is RN(x/a) (Markstein's theorem;
  * no under/overflow anywhere while |x|, |q0|, a lie in [2^-100, 2^100]).  Zero, NaN, inf and
  * extreme exponents take the IEEE sequence.  tests/test_fast_division.py checks 6e7 cases on the host
- * and 4e6 on the device (3e9 more were checked while writing it). */
+ * and 4e6 on the device (3e9 more were checked while writing it).
+ * The domain test is split so that one check per call remains: the per-ray y is NaN unless
+ * a in [2^-49, 2^49] (div_rn_y), and the call checks |q0| in [2^-50, 2^50].  Together they imply
+ * |x| = |q0 a| (1 +- 2^-23) in [2^-100, 2^100], so this domain lies inside the one above; a NaN y
+ * fails the |q0| check.  The IEEE sequence sits behind a wave vote: if-converted, every call would
+ * pay for both sequences. */
+HRT_LANE_FI float div_rn_y(float a) { return a >= 0x1p-49f && a <= 0x1p49f ? 1.0f / a : u2f(0x7fc00000u); }
 HRT_LANE_FI float div_rn(float x, float a, float y) {
   const float q0 = x * y;
-  const float q = fmaf(fmaf(-q0, a, x), y, q0);
-  const float ax = fabsf(x), aq = fabsf(q0);
-  const bool fast = ax >= 0x1p-100f && ax <= 0x1p100f && aq >= 0x1p-100f && aq <= 0x1p100f &&
-                    a >= 0x1p-100f && a <= 0x1p100f;
-  return fast ? q : x / a;
+  float q = fmaf(fmaf(-q0, a, x), y, q0);
+  const float aq = fabsf(q0);
+  const bool fast = aq >= 0x1p-50f && aq <= 0x1p50f;
+#ifndef HRT_DIV_VOTE
+#define HRT_DIV_VOTE 0 /* measured: the vote costs more than the if-converted IEEE sequence */
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && HRT_DIV_VOTE
+  if (__any(!fast)) {
+    if (!fast) q = x / a;
+  }
+#else
+  if (!fast) q = x / a;
+#endif
+  return q;
 }
 
 /* a new origin/direction; the ray keeps its time */
@@ -108,7 +124,7 @@ HRT_LANE_FI void set_dir(TRay& r, Vec3 o, Vec3 d) {
   /* aabb.rs:22 computes 1/d per call; the value is the same every time */
   r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
   r.dd = dot(d, d);
-  r.rdd = 1.0f / r.dd;
+  r.rdd = div_rn_y(r.dd);
 }
 
 HRT_LANE_FI void set_time(TRay& r, float time, const KParams& P) {
@@ -732,36 +748,47 @@ HRT_LANE_FI void init_path_state(PathState& ps) {
   ps.traced = false;
 }
 
-/* One node of the BASIC world walk (spheres and moving spheres under boxes; trace() restricted).
- * Both 16-B halves of the node are loaded and the box tested for every node kind (a PRIM node's box
- * result is ignored), so the only divergent branch is the primitive test. */
+/* One node of the BASIC world walk (spheres and moving spheres under boxes; trace() restricted),
+ * in two halves.  basic_box: both 16-B halves of the node are loaded and the box tested for every
+ * node kind (a PRIM node's box result is ignored); the walk moves on, and a primitive that must be
+ * tested is left in `pend` (its index).  basic_prim then tests it against the lane's current
+ * `closest`.  A lane runs basic_prim before its next basic_box, so its sequence of tests is exactly
+ * basic_step's (= the reference's); the kernel only chooses WHEN, batching the primitive tests of
+ * many lanes into one execution of the divergent sphere block. */
 template <int CULL, bool COUNT>
-HRT_LANE_FI void basic_step(const KParams& P, const G::Node* __restrict__ nodes,
-                                           const G::Prim* __restrict__ prims, uint32_t& i, const TRay& r,
-                                           float& closest, uint32_t& winner, Counts& cn) {
+HRT_LANE_FI void basic_box(const KParams& P, const G::Node* __restrict__ nodes, uint32_t& i, const TRay& r,
+                           float closest, uint32_t& pend, Counts& cn) {
   const G::Node* np = nodes + i;
   const float4 a = ld4(np->mn);
   const float4 b = ld4(np->mx);
   const uint32_t kp = f2u(b.w);
   const uint32_t kind = (kp >> 24) & G::KIND_MASK;
-  const float tmin = P.t_min;
   if constexpr (COUNT) cn.nodes++;
-  const bool pass = box_hit<CULL>(a, b, r, tmin, closest, (kp & G::NODE_REF_ONLY) != 0) || kind == G::K_PRIM;
+  const bool pass = box_hit<CULL>(a, b, r, P.t_min, closest, (kp & G::NODE_REF_ONLY) != 0) || kind == G::K_PRIM;
   i = pass ? i + 1 : f2u(a.w);
-  const bool test = pass && kind != G::K_BOX;
-#if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (COUNT) cn.prim_slots += __any(test) ? 1u : 0u; /* wave-level: device only */
-#endif
-  if (test) {
-    const uint32_t payload = kp & 0xFFFFFFu;
-    const G::Prim* pp = prims + payload;
-    if constexpr (COUNT) cn.prims++;
-    float t;
-    if (sphere_root(pp, pp->km & 3u, r, tmin, closest, t, P.motion_uniform != 0)) {
-      closest = t;
-      winner = payload;
-    }
+  pend = pass && kind != G::K_BOX ? (kp & 0xFFFFFFu) : G::NONE;
+}
+
+template <bool COUNT>
+HRT_LANE_FI void basic_prim(const KParams& P, const G::Prim* __restrict__ prims, uint32_t payload, const TRay& r,
+                            float& closest, uint32_t& winner, Counts& cn) {
+  const G::Prim* pp = prims + payload;
+  if constexpr (COUNT) cn.prims++;
+  float t;
+  if (sphere_root(pp, pp->km & 3u, r, P.t_min, closest, t, P.motion_uniform != 0)) {
+    closest = t;
+    winner = payload;
   }
+}
+
+/* both halves back to back (the host lane simulator's walk) */
+template <int CULL, bool COUNT>
+HRT_LANE_FI void basic_step(const KParams& P, const G::Node* __restrict__ nodes,
+                                           const G::Prim* __restrict__ prims, uint32_t& i, const TRay& r,
+                                           float& closest, uint32_t& winner, Counts& cn) {
+  uint32_t pend;
+  basic_box<CULL, COUNT>(P, nodes, i, r, closest, pend, cn);
+  if (pend != G::NONE) basic_prim<COUNT>(P, prims, pend, r, closest, winner, cn);
 }
 
 /* The BASIC kernel (sphere scenes: the Random family), with POSTPONED shading.  A lane's walk state

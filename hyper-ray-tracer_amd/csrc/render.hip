@@ -230,9 +230,14 @@ __global__ __launch_bounds__((block_threads<LDS, FAST>())) void render_kernel(KP
 }
 
 #ifndef HRT_WALK_UNROLL
-#define HRT_WALK_UNROLL 2
+#define HRT_WALK_UNROLL 6
 #endif
 constexpr int WALK_UNROLL = HRT_WALK_UNROLL; /* node steps between two checks of the wave's exit test */
+#ifndef HRT_PRIM_EVERY
+#define HRT_PRIM_EVERY HRT_WALK_UNROLL
+#endif
+constexpr int PRIM_EVERY = HRT_PRIM_EVERY; /* node steps between two checks for batched primitive tests */
+static_assert(WALK_UNROLL % PRIM_EVERY == 0, "the exit check must follow a primitive check");
 #ifndef HRT_BASIC_WAVES
 #define HRT_BASIC_WAVES 6
 #endif
@@ -259,6 +264,10 @@ void render_basic_kernel(KParams P) {
   const float inf = __uint_as_float(0x7f800000u);
   const uint32_t end = P.main_end;
   const uint32_t need = P.postpone;
+  const uint32_t batch = P.prim_batch;
+  /* watchdog: a lane's walk is at most walk_cap steps; waiting for a batch can stretch a pass to the
+   * lanes' total work (each iteration steps or tests for at least one lane) */
+  const uint32_t cap = P.walk_cap * 128u;
 
   bool has_item = false, exhausted = false;
   bool walking = false; /* a segment is in flight (walk running, or finished and waiting to shade) */
@@ -268,7 +277,7 @@ void render_basic_kernel(KParams P) {
   init_path_state(ps);
   TRay r;
   set_ray(r, ps.ro, ps.rd, 0.0f, P);
-  uint32_t node = G::NONE, winner = G::NONE;
+  uint32_t node = G::NONE, winner = G::NONE, pend = G::NONE;
   float closest = inf;
   uint32_t n_seg = 0, n_samples = 0, n_pixels = 0; /* wave totals (uniform) */
   Counts cn{0u, 0u, 0u, 0u, 0u, 0u};
@@ -294,7 +303,9 @@ void render_basic_kernel(KParams P) {
       winner = G::NONE;
       node = ps.depth_left == 0 ? G::NONE : 0u; /* max_depth 0: black without a world.hit (:478-480) */
     }
-    /* step the walks until enough lanes have finished (lanes not walking hold node >= end) */
+    /* step the walks until enough lanes have finished (lanes not walking hold node >= end).  A lane
+     * whose leaf box passed holds the primitive in `pend` and waits; the wave runs the sphere block
+     * once `batch` lanes wait (or no lane can step), instead of for every lane that needs it. */
     if constexpr (COUNT) cn.shade_slots++;
     stamp(0);
     const unsigned long long walkers = __ballot(walking);
@@ -304,11 +315,20 @@ void render_basic_kernel(KParams P) {
 #pragma unroll
       for (int u = 0; u < WALK_UNROLL; u++) {
         if constexpr (COUNT) cn.walk_slots++;
-        if (node < end) basic_step<CULL, COUNT>(P, nodes, prims, node, r, closest, winner, cn);
+        if (node < end && pend == G::NONE) basic_box<CULL, COUNT>(P, nodes, node, r, closest, pend, cn);
+        if ((u + 1) % PRIM_EVERY != 0) continue;
+        const unsigned long long pm = __ballot(pend != G::NONE);
+        if (pm && ((uint32_t)__popcll(pm) >= batch || !__ballot(node < end && pend == G::NONE))) {
+          if constexpr (COUNT) cn.prim_slots++;
+          if (pend != G::NONE) {
+            basic_prim<COUNT>(P, prims, pend, r, closest, winner, cn);
+            pend = G::NONE;
+          }
+        }
       }
-      const unsigned long long live = __ballot(node < end);
+      const unsigned long long live = __ballot(node < end || pend != G::NONE);
       if (!live || (uint32_t)__popcll(walkers & ~live) >= need) break;
-      if (++iters > P.walk_cap) { stuck = true; break; }
+      if (++iters > cap) { stuck = true; break; }
     }
     if (stuck) { /* a walk that cannot end (corrupt scene data): report it, retire the wave */
       if (lane == 0) atomicOr(&P.stats[12], 1ull);
@@ -316,10 +336,11 @@ void render_basic_kernel(KParams P) {
       has_item = false;
       walking = false;
       node = G::NONE;
+      pend = G::NONE;
     }
     stamp(1);
     /* shade the finished segments (application.rs:483-494) */
-    const bool shading = walking && node >= end;
+    const bool shading = walking && node >= end && pend == G::NONE;
     const bool traced = shading && node != G::NONE;
     bool sample_done = false, chunk_done = false;
     if (shading) {
@@ -503,7 +524,7 @@ __global__ void math_kernel(int op, const float* x, const float* y, float* out, 
     case 4: r = ln_f(a); break;
     case 5: r = pow5_f(a); break;
     case 6: r = tan_f(a); break;
-    case 7: r = div_rn(a, b, 1.0f / b); break; /* the walk's division by dot(d, d) */
+    case 7: r = div_rn(a, b, div_rn_y(b)); break; /* the walk's division by dot(d, d) */
   }
   out[i] = r;
 }
@@ -678,7 +699,8 @@ void launch_any(const hrt_scene* s, const Plan& pl, const KParams& kp, hipStream
 }
 
 /* BASIC-kernel tuning knob, 1..64 lanes (read per launch; any value gives the same image):
- *   HRT_POSTPONE   a wave leaves the walk to shade once this many lanes have finished theirs. */
+ *   HRT_POSTPONE   a wave leaves the walk to shade once this many lanes have finished theirs;
+ *   HRT_PRIM_BATCH the wave runs its primitive tests once this many lanes wait for one. */
 uint32_t env_knob(const char* name, uint32_t dflt) {
   const char* e = getenv(name);
   const long x = e ? strtol(e, nullptr, 10) : 0;
@@ -720,7 +742,8 @@ KParams scene_params(const hrt_scene* s, const hrt_camera* cam, const hrt_render
   kp.n_nodes = pl.fast ? 8 * s->f_stream_len : (uint32_t)s->g_nodes.size(); /* main stream + medium boundary subtrees */
   kp.n_prims = (uint32_t)(pl.fast ? s->f_prims.size() : s->g_prims.size());
   kp.stream_len = pl.fast ? s->f_stream_len : 0;
-  kp.postpone = env_knob("HRT_POSTPONE", 60);
+  kp.postpone = env_knob("HRT_POSTPONE", 56);
+  kp.prim_batch = env_knob("HRT_PRIM_BATCH", 3);
   /* a walk visits each node at most once, a medium's boundary subtree at most twice per medium node */
   kp.walk_cap = 3u * (uint32_t)s->g_nodes.size() + 64u;
   kp.motion_uniform = s->motion_uniform ? 1u : 0u;

@@ -18,7 +18,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libhrt.so")
+LIB_PATH = os.environ.get("HRT_LIB") or os.path.join(PKG_ROOT, "lib", "libhrt.so")  # HRT_LIB: A/B against another build
 
 # ---------------------------------------------------------------------------------------- enums
 OK = 0

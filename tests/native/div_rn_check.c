@@ -1,5 +1,7 @@
 /* Exhaustive-style check of the kernel's division by dot(d, d) (render.hip div_rn): the fma-corrected
- * quotient with a per-ray RN(1/a) must equal IEEE x / a bit for bit wherever the fast path is taken.
+ * quotient with a per-ray RN(1/a) must equal IEEE x / a bit for bit wherever the fast path is taken, and
+ * the kernel's cheaper domain test (a in [2^-49, 2^49], |q0| in [2^-50, 2^50]) may only select cases inside
+ * the proven domain.
  * Usage: div_rn_check <n> <seed> <emin> <emax>   prints "<fast-path cases> <mismatches>". */
 #include <math.h>
 #include <stdint.h>
@@ -31,8 +33,11 @@ int main(int argc, char** argv) {
     float y = yv, q = qv;
     float q0 = x * y;
     float ax = fabsf(x), aq = fabsf(q0);
-    if (!(ax >= 0x1p-100f && ax <= 0x1p100f && aq >= 0x1p-100f && aq <= 0x1p100f && a >= 0x1p-100f && a <= 0x1p100f))
-      continue;
+    int proven = ax >= 0x1p-100f && ax <= 0x1p100f && aq >= 0x1p-100f && aq <= 0x1p100f && a >= 0x1p-100f && a <= 0x1p100f;
+    /* the kernel's split test (lane.h div_rn / div_rn_y) must select a subset of the proven domain */
+    int kernel = a >= 0x1p-49f && a <= 0x1p49f && aq >= 0x1p-50f && aq <= 0x1p50f;
+    if (kernel && !proven) bad++;
+    if (!proven) continue;
     fast++;
     float got = fmaf(fmaf(-q0, a, x), y, q0);
     if (u(got) != u(q)) bad++;
