@@ -29,6 +29,14 @@ import torch  # noqa: E402  (first: libhrt binds to torch's HIP runtime)
 import hrt  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+EARTHMAP = os.path.join(ROOT, "tests", "golden", "earthmap_rgb8.png")  # the reference's assets/earthmap.jpg, decoded
+
+
+def earth_image():
+    """The texture of the Earth scenes (earth, earth_perlin, final): the reference's own asset."""
+    return hrt.load_image(EARTHMAP) if os.path.exists(EARTHMAP) else hrt.synthetic_earth()
+
+
 # algorithmic bytes of one traversal/shading step of THIS kernel (layout.h):
 NODE_B, PRIM_B, MAT_B, TEX_B, PIXEL_B = 32, 48, 32, 32, 16
 
@@ -70,7 +78,7 @@ def cpu_baseline(args, rank_segments_per_sample):
     from oracle import oracle as O
 
     threads = min(16, os.cpu_count() or 1)
-    o = O.OracleScene(hrt.PRESETS[args.preset], 1, hrt.synthetic_earth())
+    o = O.OracleScene(hrt.PRESETS[args.preset], 1, earth_image())
     W, H = args.width, args.height
     # calibrate on one row at a few spp, then size a band to ~cpu_seconds
     t0 = time.perf_counter()
@@ -115,7 +123,7 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    scene = hrt.preset(args.preset, 1, hrt.synthetic_earth())
+    scene = hrt.preset(args.preset, 1, earth_image())
     scene.commit(local)
     si = scene.scene_info()
     W, H = args.width, args.height

@@ -353,6 +353,19 @@ def synthetic_earth(width: int = 1024, height: int = 512) -> np.ndarray:
     return np.clip(img, 0, 255).astype(np.uint8)
 
 
+def load_image(path: str) -> np.ndarray:
+    """Decode an image file to the bytes hrt_tex_image takes (H x W x C uint8), as ImageTexture::new
+    does with `image::open` (image_texture.rs:19-33).  Decoding is host plumbing (Pillow here; the
+    Rust host keeps `image`): the ABI itself takes decoded bytes."""
+    from PIL import Image
+
+    im = Image.open(path)
+    if im.mode not in ("L", "LA", "RGB", "RGBA"):
+        im = im.convert("RGB")
+    a = np.asarray(im, dtype=np.uint8)
+    return np.ascontiguousarray(a[..., None] if a.ndim == 2 else a)
+
+
 def preset(name_or_id, scene_seed: int = 1, image: Optional[np.ndarray] = None) -> Scene:
     """Build one of the reference scenes (application.rs:497-935) with a seeded builder stream."""
     pid = PRESETS[name_or_id] if isinstance(name_or_id, str) else int(name_or_id)

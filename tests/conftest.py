@@ -16,8 +16,14 @@ def pytest_configure(config):
                                        "(run explicitly with -m gpu_wip)")
 
 
+EARTHMAP = os.path.join(ROOT, "tests", "golden", "earthmap_rgb8.png")
+
+
 @pytest.fixture(scope="session")
 def earth():
+    """The reference's own texture (assets/earthmap.jpg, decoded by tests/golden/make_earthmap.py)."""
     import hrt
 
-    return hrt.synthetic_earth()
+    img = hrt.load_image(EARTHMAP)
+    assert img.shape == (512, 1024, 3)
+    return img
