@@ -202,6 +202,60 @@ HRT_LANE_FI bool box_hit(const float4& a, const float4& b, const TRay& r, float 
   return ok & (ref_only | !(hi < lo));
 }
 
+/* The two halves of CULL_EXACT on their own, for the sphere-scene walk (basic_box / basic_prim).
+ *
+ * The reference test is MONOTONE under box inclusion: a BVH box contains its children's boxes
+ * (Aabb::surrounding_box), so per axis a child's [ts, te] lies inside its parent's (the products
+ * (mn - o) * inv round monotonically; a NaN axis, 0 * inf, passes as "no constraint" for every box
+ * with that face, see box_hit), and closest only shrinks along the walk.  So if the reference fails an
+ * inner node, it fails every leaf below it, at any later closest.  The walk can therefore apply the
+ * reference test at LEAVES only (right before the primitive test) and cull inner nodes with the
+ * inflated test alone: it tests exactly the primitives the exact walk tests, in the same order, with
+ * the same closest. */
+HRT_LANE_FI bool box_ref(const float4& a, const float4& b, const TRay& r, float tmin, float tmax) {
+  const float mn[3] = {a.x, a.y, a.z}, mx[3] = {b.x, b.y, b.z};
+  const float o[3] = {r.o.x, r.o.y, r.o.z}, inv[3] = {r.inv.x, r.inv.y, r.inv.z};
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const float t0 = (mn[k] - o[k]) * inv[k], t1 = (mx[k] - o[k]) * inv[k];
+    const bool neg = inv[k] < 0.0f; /* aabb.rs:28-29 */
+    const float ts = neg ? t1 : t0, te = neg ? t0 : t1;
+    ok = ok & !(fminf(te, tmax) <= fmaxf(ts, tmin));
+  }
+  return ok;
+}
+
+/* The inflated slab test of CULL_EXACT alone: false only if the box, widened by EXACT_MARGIN x its
+ * L-inf distance D, misses the ray on [tmin, tmax].  The widening w = margin |inv_k| is folded into
+ * one fma per bound (one rounding instead of two; rounding errors ~1e-7 D are far inside the 1.65x
+ * slack of EXACT_MARGIN).  A NaN bound (0 * inf) is ignored by fmaxf/fminf: no constraint. */
+HRT_LANE_FI bool box_infl(const float4& a, const float4& b, const TRay& r, float tmin, float tmax) {
+  const float mn[3] = {a.x, a.y, a.z}, mx[3] = {b.x, b.y, b.z};
+  const float o[3] = {r.o.x, r.o.y, r.o.z}, inv[3] = {r.inv.x, r.inv.y, r.inv.z};
+  float dmn[3], dmx[3], ts[3], te[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    dmn[k] = mn[k] - o[k];
+    dmx[k] = mx[k] - o[k];
+    const float t0 = dmn[k] * inv[k], t1 = dmx[k] * inv[k];
+    const bool neg = inv[k] < 0.0f;
+    ts[k] = neg ? t1 : t0;
+    te[k] = neg ? t0 : t1;
+  }
+  float dist = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 3; k++) dist = fmaxf(dist, fmaxf(fabsf(dmn[k]), fabsf(dmx[k])));
+  const float margin = G::EXACT_MARGIN * dist;
+  float lo = tmin, hi = tmax;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    lo = fmaxf(lo, fmaf(-margin, fabsf(inv[k]), ts[k]));
+    hi = fminf(hi, fmaf(margin, fabsf(inv[k]), te[k]));
+  }
+  return !(hi < lo);
+}
+
 /* sphere.rs:38-55 / moving_sphere.rs:61-78: the accepted root only */
 HRT_LANE_FI bool sphere_root(const G::Prim* pp, uint32_t kind, const TRay& r, float tmin,
                                             float tmax, float& root, bool motion_uniform) {
@@ -750,11 +804,15 @@ HRT_LANE_FI void init_path_state(PathState& ps) {
 
 /* One node of the BASIC world walk (spheres and moving spheres under boxes; trace() restricted),
  * in two halves.  basic_box: both 16-B halves of the node are loaded and the box tested for every
- * node kind (a PRIM node's box result is ignored); the walk moves on, and a primitive that must be
- * tested is left in `pend` (its index).  basic_prim then tests it against the lane's current
- * `closest`.  A lane runs basic_prim before its next basic_box, so its sequence of tests is exactly
- * basic_step's (= the reference's); the kernel only chooses WHEN, batching the primitive tests of
- * many lanes into one execution of the divergent sphere block. */
+ * node kind (a PRIM node's box result is ignored); the walk moves on (a passed node's successor is
+ * node + 1, so the leaf is found again as i - 1), and a primitive that must be tested is left in
+ * `pend` (its index).  basic_prim then tests it against the lane's current `closest`.  A lane runs
+ * basic_prim before its next basic_box, so its sequence of tests is exactly basic_step's; the kernel
+ * only chooses WHEN, batching the primitive tests of many lanes into one execution of the divergent
+ * sphere block.
+ * Under CULL_EXACT, basic_box applies the inflated test alone and basic_prim applies the reference
+ * test to the leaf's box first (box_ref: the reference test is monotone, so leaves suffice); the
+ * other modes test the whole box in basic_box. */
 template <int CULL, bool COUNT>
 HRT_LANE_FI void basic_box(const KParams& P, const G::Node* __restrict__ nodes, uint32_t& i, const TRay& r,
                            float closest, uint32_t& pend, Counts& cn) {
@@ -764,14 +822,25 @@ HRT_LANE_FI void basic_box(const KParams& P, const G::Node* __restrict__ nodes, 
   const uint32_t kp = f2u(b.w);
   const uint32_t kind = (kp >> 24) & G::KIND_MASK;
   if constexpr (COUNT) cn.nodes++;
-  const bool pass = box_hit<CULL>(a, b, r, P.t_min, closest, (kp & G::NODE_REF_ONLY) != 0) || kind == G::K_PRIM;
+  bool pass;
+  if constexpr (CULL == G::CULL_EXACT)
+    pass = box_infl(a, b, r, P.t_min, closest) || (kp & G::NODE_REF_ONLY) != 0 || kind == G::K_PRIM;
+  else
+    pass = box_hit<CULL>(a, b, r, P.t_min, closest) || kind == G::K_PRIM;
   i = pass ? i + 1 : f2u(a.w);
   pend = pass && kind != G::K_BOX ? (kp & 0xFFFFFFu) : G::NONE;
 }
 
-template <bool COUNT>
-HRT_LANE_FI void basic_prim(const KParams& P, const G::Prim* __restrict__ prims, uint32_t payload, const TRay& r,
-                            float& closest, uint32_t& winner, Counts& cn) {
+/* `leaf` = the node that left `payload` pending (the walk's i - 1) */
+template <int CULL, bool COUNT>
+HRT_LANE_FI void basic_prim(const KParams& P, const G::Node* __restrict__ nodes, const G::Prim* __restrict__ prims,
+                            uint32_t leaf, uint32_t payload, const TRay& r, float& closest, uint32_t& winner,
+                            Counts& cn) {
+  if constexpr (CULL == G::CULL_EXACT) {
+    const G::Node* np = nodes + leaf;
+    const float4 b = ld4(np->mx);
+    if (((f2u(b.w) >> 24) & G::KIND_MASK) != G::K_PRIM && !box_ref(ld4(np->mn), b, r, P.t_min, closest)) return;
+  }
   const G::Prim* pp = prims + payload;
   if constexpr (COUNT) cn.prims++;
   float t;
@@ -788,7 +857,7 @@ HRT_LANE_FI void basic_step(const KParams& P, const G::Node* __restrict__ nodes,
                                            float& closest, uint32_t& winner, Counts& cn) {
   uint32_t pend;
   basic_box<CULL, COUNT>(P, nodes, i, r, closest, pend, cn);
-  if (pend != G::NONE) basic_prim<COUNT>(P, prims, pend, r, closest, winner, cn);
+  if (pend != G::NONE) basic_prim<CULL, COUNT>(P, nodes, prims, i - 1u, pend, r, closest, winner, cn);
 }
 
 /* The BASIC kernel (sphere scenes: the Random family), with POSTPONED shading.  A lane's walk state

@@ -321,7 +321,7 @@ void render_basic_kernel(KParams P) {
         if (pm && ((uint32_t)__popcll(pm) >= batch || !__ballot(node < end && pend == G::NONE))) {
           if constexpr (COUNT) cn.prim_slots++;
           if (pend != G::NONE) {
-            basic_prim<COUNT>(P, prims, pend, r, closest, winner, cn);
+            basic_prim<CULL, COUNT>(P, nodes, prims, node - 1u, pend, r, closest, winner, cn);
             pend = G::NONE;
           }
         }

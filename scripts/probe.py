@@ -22,7 +22,8 @@ ap.add_argument("--env", default="", help="/-list of NAME=VALUE[,NAME=VALUE] env
 ap.add_argument("--count", action="store_true", help="also run one instrumented pass per variant")
 a = ap.parse_args()
 
-s = hrt.preset(a.preset, 1)
+_earth = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden", "earthmap_rgb8.png")
+s = hrt.preset(a.preset, 1, hrt.load_image(_earth) if os.path.exists(_earth) else None)
 s.commit(0)
 si = s.scene_info()
 print(f"scene {a.preset}: nodes {si.nodes} prims {si.prims} features {si.feature_mask:#x} cull {si.cull_mode} blob {si.blob_bytes} B", flush=True)
