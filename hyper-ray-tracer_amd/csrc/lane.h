@@ -725,14 +725,20 @@ HRT_LANE_FI bool shade(const KParams& P, PathState& ps, uint32_t winner, float c
   bool scattered = false;
   Rng& rng = ps.rng;
   bool textured = false; /* att (or, for a light, emitted) = the material's texture at the hit */
+  /* Lambertian, Metal and Isotropic each start with random_in_unit_sphere (their first draws; Metal's
+   * reflect draws nothing): ONE rejection loop shared by the three branches, so a wave holding several
+   * of these materials runs the loop once, not once per branch. */
+  Vec3 sph = v3(0.0f, 0.0f, 0.0f);
+  if (M.kind == G::M_LAMBERTIAN || M.kind == G::M_METAL || (FULL && M.kind == G::M_ISOTROPIC))
+    sph = random_in_unit_sphere(rng);
   if (M.kind == G::M_LAMBERTIAN) { /* lambertian.rs:27-38 */
-    ndir = rec.n + random_unit_vector(rng);
+    ndir = rec.n + normalize(sph); /* random_unit_vector, math.rs:12-14 */
     if (near_zero(ndir)) ndir = rec.n;
     textured = true;
     scattered = true;
   } else if (M.kind == G::M_METAL) { /* metal.rs:29-42 */
     Vec3 reflected = reflect(normalize(rd), rec.n);
-    ndir = reflected + M.a[3] * random_in_unit_sphere(rng);
+    ndir = reflected + M.a[3] * sph;
     scattered = dot(ndir, rec.n) > 0.0f;
     att = v3(M.a[0], M.a[1], M.a[2]);
   } else if (M.kind == G::M_DIELECTRIC) { /* dielectric.rs:31-55 */
@@ -748,7 +754,7 @@ HRT_LANE_FI bool shade(const KParams& P, PathState& ps, uint32_t winner, float c
   } else if (FULL && M.kind == G::M_DIFFUSE_LIGHT) { /* diffuse_light.rs:20-28 */
     textured = true;
   } else if (FULL && M.kind == G::M_ISOTROPIC) { /* isotropic.rs:26-33 */
-    ndir = random_in_unit_sphere(rng);
+    ndir = sph;
     textured = true;
     scattered = true;
   }
