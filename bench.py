@@ -70,6 +70,12 @@ def host_cpu():
     return "unknown"
 
 
+def log(msg):
+    """Progress on stderr (stdout carries only the JSON line)."""
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_baseline(args, rank_segments_per_sample):
     """The CPU restatement of the reference path (oracle/, 'port'), 80x80 tiles on a thread pool,
     timed on this host on a bounded band of the same frame (rows through the middle of the image),
@@ -140,8 +146,12 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     # exact work of one step: segments are deterministic for a fixed seed and sample range
+    tw = time.perf_counter()
     st = hrt.render_tiles_device(scene, cam, p, tiles, out.data_ptr(), stream.cuda_stream, want_stats=True)
     seg_step, samples_step = int(st.segments), int(st.samples)
+    warm_s = time.perf_counter() - tw
+    progress = warm_s > 20.0  # long frames: a progress line per timed frame
+    log(f"warm-up frame: {seg_step} rays in {warm_s:.1f} s")
     for _ in range(max(0, args.warmup - 1)):
         hrt.render_tiles_device(scene, cam, p, tiles, out.data_ptr(), stream.cuda_stream)
 
@@ -157,6 +167,9 @@ def main():
         ev[k][0].record(stream)
         hrt.render_tiles_device(scene, cam, p, tiles, out.data_ptr(), stream.cuda_stream)
         ev[k][1].record(stream)
+        if progress and k + 1 < args.steps:
+            ev[k][1].synchronize()  # progress line per frame (long configs); the clock keeps running
+            log(f"timed frame {k + 1}/{args.steps}")
     torch.cuda.synchronize(dev)
     barrier()
     dt = time.perf_counter() - t0
