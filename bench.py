@@ -70,6 +70,20 @@ def host_cpu():
     return "unknown"
 
 
+SCENE_LABEL = {  # BASELINE.json configs
+    "random": "RTIOW random spheres",
+    "earth_perlin": "Earth-mapped sphere over a Perlin-noise ground",
+    "random_10k": "10k random spheres, deep BVH",
+    "cornell": "Next-Week Cornell box",
+    "final": "Next-Week final scene",
+}
+SCENE_DATA = {
+    "random": "synthetic (seeded Scene::Random builder; no external assets)",
+    "earth_perlin": "seeded builder; the reference's assets/earthmap.jpg (tests/golden/earthmap_rgb8.png)",
+    "final": "seeded builder; the reference's assets/earthmap.jpg (tests/golden/earthmap_rgb8.png)",
+}
+
+
 def log(msg):
     """Progress on stderr (stdout carries only the JSON line)."""
     if int(os.environ.get("RANK", "0")) == 0:
@@ -244,9 +258,9 @@ def main():
             "scaling": "weak" if world == 1 or args.scaling == "weak" else "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded Scene::Random builder; no external assets)",
+            "data": SCENE_DATA.get(args.preset, "synthetic (seeded scene builder)"),
             "config": {
-                "workload": f"Scene::{args.preset} (RTIOW random spheres) {W}x{H}, {args.spp} spp, max_depth {args.depth}",
+                "workload": f"Scene::{args.preset} ({SCENE_LABEL.get(args.preset, args.preset)}) {W}x{H}, {args.spp} spp, max_depth {args.depth}",
                 "width": W, "height": H, "spp": args.spp, "max_depth": args.depth,
                 "rays_per_step": int(seg_all), "samples_per_step": int(samples_all),
                 "rays_per_sample": round(seg_all / max(1.0, samples_all), 4),

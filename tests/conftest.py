@@ -12,8 +12,6 @@ sys.path.insert(0, ROOT)
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an AMD GPU (MI355X); runs via gpurun")
     config.addinivalue_line("markers", "slow: long-running CPU test")
-    config.addinivalue_line("markers", "gpu_wip: GPU test of an opt-in kernel not yet validated on hardware "
-                                       "(run explicitly with -m gpu_wip)")
 
 
 EARTHMAP = os.path.join(ROOT, "tests", "golden", "earthmap_rgb8.png")

@@ -31,7 +31,7 @@ def test_c_example_fails_loudly_without_a_device(exe, tmp_path):
     assert not (tmp_path / "x.ppm").exists()
 
 
-@pytest.mark.gpu_wip
+@pytest.mark.gpu
 @pytest.mark.skipif(not _has_gpu(), reason="needs a GPU")
 def test_c_example_renders(exe, tmp_path):
     out = tmp_path / "r.ppm"

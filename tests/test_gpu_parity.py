@@ -196,7 +196,7 @@ def _has_gpu():
     return torch.cuda.is_available()
 
 
-@pytest.mark.gpu_wip
+@pytest.mark.gpu
 @pytest.mark.skipif(not _has_gpu(), reason="needs a GPU")
 @pytest.mark.parametrize("name,w,h,spp", [("cornell", 40, 40, 16), ("cornell_smoke", 40, 40, 16), ("final", 40, 40, 8),
                                           ("features", 64, 36, 16), ("earth_perlin", 48, 27, 16), ("simple_light", 48, 27, 16)])
@@ -215,7 +215,7 @@ def test_persistent_general_kernel_equals_segment_kernel(earth, monkeypatch, nam
     assert np.array_equal(a, b)
 
 
-@pytest.mark.gpu_wip
+@pytest.mark.gpu
 @pytest.mark.skipif(not _has_gpu(), reason="needs a GPU")
 @pytest.mark.parametrize("batch,world", [(1, 1), (5, 1), (64, 1), (3, 2)])
 def test_progressive_tiles_assemble_the_frame(earth, batch, world):
