@@ -186,8 +186,20 @@ __device__ __forceinline__ void flush_stats(const KParams& P, uint32_t n_seg, ui
 
 /* The general kernel (every feature): each iteration of the wave loop advances every busy lane by
  * exactly one ray segment.  Lanes whose path ended start their next sample in the same iteration. */
+#ifndef HRT_GEN_WAVES
+#define HRT_GEN_WAVES 0 /* waves/SIMD cap of the general (FULL) segment kernel; 0 = compiler's choice */
+#endif
+template <bool FULL, bool LDS, bool FAST>
+constexpr int general_min_waves() { return FULL && HRT_GEN_WAVES > 0 ? HRT_GEN_WAVES : 1; }
+
+/* the FULL segment kernel needs ~140 VGPRs (3 waves/SIMD): 256-thread workgroups, so that three of
+ * them (each with its own LDS copy of a small scene) fill a CU */
+template <bool FULL, bool LDS, bool FAST>
+constexpr int general_block_threads() { return FULL ? 256 : block_threads<LDS, FAST>(); }
+
 template <int CULL, bool FULL, bool COUNT, bool LDS, bool FAST>
-__global__ __launch_bounds__((block_threads<LDS, FAST>())) void render_kernel(KParams P) {
+__global__ __launch_bounds__((general_block_threads<FULL, LDS, FAST>()), (general_min_waves<FULL, LDS, FAST>()))
+void render_kernel(KParams P) {
   extern __shared__ float4 lds_scene[];
   const G::Node* nodes = P.nodes;
   const G::Prim* prims = P.prims;
@@ -598,7 +610,7 @@ int resident_grid(const void* fn, int block, int device, size_t smem, bool lds) 
 template <int CULL, bool FULL, bool COUNT, bool LDS, bool FAST>
 void launch(const KParams& kp, int device, hipStream_t stream, size_t smem) {
   const void* fn = (const void*)render_kernel<CULL, FULL, COUNT, LDS, FAST>;
-  const int block = block_threads<LDS, FAST>();
+  const int block = general_block_threads<FULL, LDS, FAST>();
   const int grid = resident_grid(fn, block, device, LDS ? smem : 0, LDS);
   hipLaunchKernelGGL((render_kernel<CULL, FULL, COUNT, LDS, FAST>), dim3(grid), dim3(block), LDS ? smem : 0, stream,
                      kp);
@@ -627,6 +639,7 @@ void launch_basic(const KParams& kp, int device, hipStream_t stream, size_t smem
  * 160 KiB), the 8 SAH octant streams once (one 1024-thread workgroup). */
 constexpr size_t LDS_SCENE_MAX = 72 * 1024;
 constexpr size_t LDS_FAST_MAX = 150 * 1024;
+constexpr size_t LDS_GEN_MAX = 48 * 1024;
 
 struct Plan {
   bool full, fast, lds;
@@ -656,7 +669,10 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
    * scenes can be sent to the segment kernel for diagnostics (HRT_KERNEL=general). */
   const bool persistent = k && strcmp(k, "persistent") == 0;
   pl.general = (k && strcmp(k, "general") == 0) || s->media_nested || (pl.full && !persistent);
-  if (pl.general && pl.full) pl.lds = false; /* render_kernel<FULL> reads the scene from global memory */
+  /* render_kernel<FULL>: node stream + primitives in LDS when they fit three 256-thread workgroups per
+   * CU (HRT_GEN_LDS=0: global memory, for A/B) */
+  const char* gl = getenv("HRT_GEN_LDS");
+  if (pl.general && pl.full && (pl.smem > LDS_GEN_MAX || (gl && strcmp(gl, "0") == 0))) pl.lds = false;
   return pl;
 }
 
@@ -669,9 +685,12 @@ void launch_any(const hrt_scene* s, const Plan& pl, const KParams& kp, hipStream
   } else if (pl.general) {
     const int c = pl.cull;
     if (pl.full) {
-      if (c == G::CULL_EXACT) launch<G::CULL_EXACT, true, COUNT, false, false>(kp, s->device, stream, 0);
-      else if (c == G::CULL_SLAB) launch<G::CULL_SLAB, true, COUNT, false, false>(kp, s->device, stream, 0);
-      else launch<G::CULL_REFERENCE, true, COUNT, false, false>(kp, s->device, stream, 0);
+      if (c == G::CULL_EXACT) pl.lds ? launch<G::CULL_EXACT, true, COUNT, true, false>(kp, s->device, stream, smem)
+                                     : launch<G::CULL_EXACT, true, COUNT, false, false>(kp, s->device, stream, 0);
+      else if (c == G::CULL_SLAB) pl.lds ? launch<G::CULL_SLAB, true, COUNT, true, false>(kp, s->device, stream, smem)
+                                         : launch<G::CULL_SLAB, true, COUNT, false, false>(kp, s->device, stream, 0);
+      else pl.lds ? launch<G::CULL_REFERENCE, true, COUNT, true, false>(kp, s->device, stream, smem)
+                  : launch<G::CULL_REFERENCE, true, COUNT, false, false>(kp, s->device, stream, 0);
       return;
     }
     if (c == G::CULL_EXACT) pl.lds ? launch<G::CULL_EXACT, false, COUNT, true, false>(kp, s->device, stream, smem)
