@@ -231,6 +231,27 @@ HRT_LANE_FI bool box_ref(const float4& a, const float4& b, const TRay& r, float 
  * one fma per bound (one rounding instead of two; rounding errors ~1e-7 D are far inside the 1.65x
  * slack of EXACT_MARGIN).  A NaN bound (0 * inf) is ignored by fmaxf/fminf: no constraint. */
 HRT_LANE_FI bool box_infl(const float4& a, const float4& b, const TRay& r, float tmin, float tmax) {
+#if HRT_EXP_PK && defined(__HIP_DEVICE_COMPILE__)
+  /* x and y as packed pairs (v_pk_add/mul/fma_f32: two IEEE operations per issue), z alone */
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 oxy = {r.o.x, r.o.y}, ixy = {r.inv.x, r.inv.y};
+  const f2 dmn = f2{a.x, a.y} - oxy, dmx = f2{b.x, b.y} - oxy;
+  const f2 t0 = dmn * ixy, t1 = dmx * ixy;
+  const float dmnz = a.z - r.o.z, dmxz = b.z - r.o.z;
+  const float t0z = dmnz * r.inv.z, t1z = dmxz * r.inv.z;
+  const f2 ts = {r.inv.x < 0.0f ? t1.x : t0.x, r.inv.y < 0.0f ? t1.y : t0.y};
+  const f2 te = {r.inv.x < 0.0f ? t0.x : t1.x, r.inv.y < 0.0f ? t0.y : t1.y};
+  const float tsz = r.inv.z < 0.0f ? t1z : t0z, tez = r.inv.z < 0.0f ? t0z : t1z;
+  const float dist = fmaxf(fmaxf(fmaxf(fabsf(dmn.x), fabsf(dmx.x)), fmaxf(fabsf(dmn.y), fabsf(dmx.y))),
+                           fmaxf(fabsf(dmnz), fabsf(dmxz)));
+  const float margin = G::EXACT_MARGIN * dist;
+  const f2 aixy = {fabsf(r.inv.x), fabsf(r.inv.y)};
+  const f2 lo2 = __builtin_elementwise_fma(f2{-margin, -margin}, aixy, ts);
+  const f2 hi2 = __builtin_elementwise_fma(f2{margin, margin}, aixy, te);
+  const float lo = fmaxf(fmaxf(fmaxf(tmin, lo2.x), lo2.y), fmaf(-margin, fabsf(r.inv.z), tsz));
+  const float hi = fminf(fminf(fminf(tmax, hi2.x), hi2.y), fmaf(margin, fabsf(r.inv.z), tez));
+  return !(hi < lo);
+#else
   const float mn[3] = {a.x, a.y, a.z}, mx[3] = {b.x, b.y, b.z};
   const float o[3] = {r.o.x, r.o.y, r.o.z}, inv[3] = {r.inv.x, r.inv.y, r.inv.z};
   float dmn[3], dmx[3], ts[3], te[3];
@@ -254,6 +275,7 @@ HRT_LANE_FI bool box_infl(const float4& a, const float4& b, const TRay& r, float
     hi = fminf(hi, fmaf(margin, fabsf(inv[k]), te[k]));
   }
   return !(hi < lo);
+#endif
 }
 
 /* sphere.rs:38-55 / moving_sphere.rs:61-78: the accepted root only */
