@@ -268,13 +268,20 @@ HRT_LANE_FI bool box_infl(const float4& a, const float4& b, const TRay& r, float
 #pragma unroll
   for (int k = 0; k < 3; k++) dist = fmaxf(dist, fmaxf(fabsf(dmn[k]), fabsf(dmx[k])));
   const float margin = G::EXACT_MARGIN * dist;
-  float lo = tmin, hi = tmax;
+  /* !(min(tmax, h0, h1, h2) < max(tmin, l0, l1, l2)) with NaN bounds ignored, i.e. no pair
+   * (lower, upper) out of order, written as three comparisons: the widened bounds come from fmas
+   * (canonical), so max3/min3 need no quieting, and tmin / tmax only meet comparisons (fmaxf/fminf on
+   * them cost a canonicalising v_max per operand per node step).  The fourth pair, tmin <= tmax, holds
+   * on every walk (tmax is +inf or an accepted root >= tmin). */
+  float l[3], h[3];
 #pragma unroll
   for (int k = 0; k < 3; k++) {
-    lo = fmaxf(lo, fmaf(-margin, fabsf(inv[k]), ts[k]));
-    hi = fminf(hi, fmaf(margin, fabsf(inv[k]), te[k]));
+    l[k] = fmaf(-margin, fabsf(inv[k]), ts[k]);
+    h[k] = fmaf(margin, fabsf(inv[k]), te[k]);
   }
-  return !(hi < lo);
+  const float lo = fmaxf(fmaxf(l[0], l[1]), l[2]); /* NaN only if all three are: no constraint */
+  const float hi = fminf(fminf(h[0], h[1]), h[2]);
+  return !(hi < lo) & !(hi < tmin) & !(tmax < lo);
 #endif
 }
 
@@ -841,34 +848,52 @@ HRT_LANE_FI void init_path_state(PathState& ps) {
  * Under CULL_EXACT, basic_box applies the inflated test alone and basic_prim applies the reference
  * test to the leaf's box first (box_ref: the reference test is monotone, so leaves suffice); the
  * other modes test the whole box in basic_box. */
+/* The walk position of the BASIC kernel is ONE register: the next node's index, with WALK_PEND set
+ * while the primitive of the leaf just passed (index - 1) waits for its test, or NONE when the lane
+ * has no walk.  So "can step" is the single compare i < end, and the waiting primitive is read back
+ * from the leaf's own record (basic_prim loads that record anyway for the reference test). */
+constexpr uint32_t WALK_PEND = 1u << 31;
+HRT_LANE_FI bool walk_pending(uint32_t i) { return i - WALK_PEND < 0x7FFFFFFFu; } /* PEND set, i != NONE */
+
+/* A BASIC scene holds K_BOX, K_BOX_PRIM and K_PRIM nodes only (F_BASIC: no instances or media), so
+ * kp >= K_PRIM << 24 holds exactly for the nodes the inflated test must pass: K_PRIM (no box) and
+ * NODE_REF_ONLY (bit 31). */
 template <int CULL, bool COUNT>
 HRT_LANE_FI void basic_box(const KParams& P, const G::Node* __restrict__ nodes, uint32_t& i, const TRay& r,
-                           float closest, uint32_t& pend, Counts& cn) {
+                           float closest, Counts& cn) {
   const G::Node* np = nodes + i;
   const float4 a = ld4(np->mn);
   const float4 b = ld4(np->mx);
+  uint32_t skip = f2u(a.w);
+#if defined(__HIP_DEVICE_COMPILE__)
+  /* keep the skip link in the node's first 16-B load: left to itself the compiler narrows that load
+   * to 12 B and fetches the link in a second, dependent LDS read on the fail path */
+  asm("" : "+v"(skip));
+#endif
   const uint32_t kp = f2u(b.w);
-  const uint32_t kind = (kp >> 24) & G::KIND_MASK;
   if constexpr (COUNT) cn.nodes++;
   bool pass;
   if constexpr (CULL == G::CULL_EXACT)
-    pass = box_infl(a, b, r, P.t_min, closest) || (kp & G::NODE_REF_ONLY) != 0 || kind == G::K_PRIM;
+    pass = box_infl(a, b, r, P.t_min, closest) || kp >= (G::K_PRIM << 24);
   else
-    pass = box_hit<CULL>(a, b, r, P.t_min, closest) || kind == G::K_PRIM;
-  i = pass ? i + 1 : f2u(a.w);
-  pend = pass && kind != G::K_BOX ? (kp & 0xFFFFFFu) : G::NONE;
+    pass = box_hit<CULL>(a, b, r, P.t_min, closest) || ((kp >> 24) & G::KIND_MASK) == G::K_PRIM;
+  const bool prim = (kp & (G::KIND_MASK << 24)) != 0u; /* K_BOX_PRIM or K_PRIM: a primitive to test */
+  const uint32_t next = i + (prim ? 1u + WALK_PEND : 1u);
+  i = pass ? next : skip;
 }
 
-/* `leaf` = the node that left `payload` pending (the walk's i - 1) */
+/* i = the walk position with WALK_PEND set; clears it and tests the leaf (i - 1)'s primitive */
 template <int CULL, bool COUNT>
 HRT_LANE_FI void basic_prim(const KParams& P, const G::Node* __restrict__ nodes, const G::Prim* __restrict__ prims,
-                            uint32_t leaf, uint32_t payload, const TRay& r, float& closest, uint32_t& winner,
-                            Counts& cn) {
+                            uint32_t& i, const TRay& r, float& closest, uint32_t& winner, Counts& cn) {
+  i -= WALK_PEND;
+  const G::Node* np = nodes + (i - 1u);
+  const float4 b = ld4(np->mx);
+  const uint32_t kp = f2u(b.w);
   if constexpr (CULL == G::CULL_EXACT) {
-    const G::Node* np = nodes + leaf;
-    const float4 b = ld4(np->mx);
-    if (((f2u(b.w) >> 24) & G::KIND_MASK) != G::K_PRIM && !box_ref(ld4(np->mn), b, r, P.t_min, closest)) return;
+    if (((kp >> 24) & G::KIND_MASK) != G::K_PRIM && !box_ref(ld4(np->mn), b, r, P.t_min, closest)) return;
   }
+  const uint32_t payload = kp & 0xFFFFFFu;
   const G::Prim* pp = prims + payload;
   if constexpr (COUNT) cn.prims++;
   float t;
@@ -883,9 +908,8 @@ template <int CULL, bool COUNT>
 HRT_LANE_FI void basic_step(const KParams& P, const G::Node* __restrict__ nodes,
                                            const G::Prim* __restrict__ prims, uint32_t& i, const TRay& r,
                                            float& closest, uint32_t& winner, Counts& cn) {
-  uint32_t pend;
-  basic_box<CULL, COUNT>(P, nodes, i, r, closest, pend, cn);
-  if (pend != G::NONE) basic_prim<CULL, COUNT>(P, nodes, prims, i - 1u, pend, r, closest, winner, cn);
+  basic_box<CULL, COUNT>(P, nodes, i, r, closest, cn);
+  if (walk_pending(i)) basic_prim<CULL, COUNT>(P, nodes, prims, i, r, closest, winner, cn);
 }
 
 /* The BASIC kernel (sphere scenes: the Random family), with POSTPONED shading.  A lane's walk state

@@ -289,7 +289,7 @@ void render_basic_kernel(KParams P) {
   init_path_state(ps);
   TRay r;
   set_ray(r, ps.ro, ps.rd, 0.0f, P);
-  uint32_t node = G::NONE, winner = G::NONE, pend = G::NONE;
+  uint32_t node = G::NONE, winner = G::NONE; /* node: walk position (basic_box: index | WALK_PEND, or NONE) */
   float closest = inf;
   uint32_t n_seg = 0, n_samples = 0, n_pixels = 0; /* wave totals (uniform) */
   Counts cn{0u, 0u, 0u, 0u, 0u, 0u};
@@ -316,7 +316,7 @@ void render_basic_kernel(KParams P) {
       node = ps.depth_left == 0 ? G::NONE : 0u; /* max_depth 0: black without a world.hit (:478-480) */
     }
     /* step the walks until enough lanes have finished (lanes not walking hold node >= end).  A lane
-     * whose leaf box passed holds the primitive in `pend` and waits; the wave runs the sphere block
+     * whose leaf box passed holds WALK_PEND in `node` and waits; the wave runs the sphere block
      * once `batch` lanes wait (or no lane can step), instead of for every lane that needs it. */
     if constexpr (COUNT) cn.shade_slots++;
     stamp(0);
@@ -327,18 +327,16 @@ void render_basic_kernel(KParams P) {
 #pragma unroll
       for (int u = 0; u < WALK_UNROLL; u++) {
         if constexpr (COUNT) cn.walk_slots++;
-        if (node < end && pend == G::NONE) basic_box<CULL, COUNT>(P, nodes, node, r, closest, pend, cn);
+        if (node < end) basic_box<CULL, COUNT>(P, nodes, node, r, closest, cn);
         if ((u + 1) % PRIM_EVERY != 0) continue;
-        const unsigned long long pm = __ballot(pend != G::NONE);
-        if (pm && ((uint32_t)__popcll(pm) >= batch || !__ballot(node < end && pend == G::NONE))) {
+        const bool waiting = walk_pending(node);
+        const unsigned long long pm = __ballot(waiting);
+        if (pm && ((uint32_t)__popcll(pm) >= batch || !__ballot(node < end))) {
           if constexpr (COUNT) cn.prim_slots++;
-          if (pend != G::NONE) {
-            basic_prim<CULL, COUNT>(P, nodes, prims, node - 1u, pend, r, closest, winner, cn);
-            pend = G::NONE;
-          }
+          if (waiting) basic_prim<CULL, COUNT>(P, nodes, prims, node, r, closest, winner, cn);
         }
       }
-      const unsigned long long live = __ballot(node < end || pend != G::NONE);
+      const unsigned long long live = __ballot(node < end || walk_pending(node));
       if (!live || (uint32_t)__popcll(walkers & ~live) >= need) break;
       if (++iters > cap) { stuck = true; break; }
     }
@@ -348,11 +346,10 @@ void render_basic_kernel(KParams P) {
       has_item = false;
       walking = false;
       node = G::NONE;
-      pend = G::NONE;
     }
     stamp(1);
     /* shade the finished segments (application.rs:483-494) */
-    const bool shading = walking && node >= end && pend == G::NONE;
+    const bool shading = walking && node >= end && !walk_pending(node);
     const bool traced = shading && node != G::NONE;
     bool sample_done = false, chunk_done = false;
     if (shading) {
