@@ -759,7 +759,7 @@ KParams scene_params(const hrt_scene* s, const hrt_camera* cam, const hrt_render
   kp.n_prims = (uint32_t)(pl.fast ? s->f_prims.size() : s->g_prims.size());
   kp.stream_len = pl.fast ? s->f_stream_len : 0;
   kp.postpone = env_knob("HRT_POSTPONE", 56);
-  kp.prim_batch = env_knob("HRT_PRIM_BATCH", 4);
+  kp.prim_batch = env_knob("HRT_PRIM_BATCH", 8);
   /* a walk visits each node at most once, a medium's boundary subtree at most twice per medium node */
   kp.walk_cap = 3u * (uint32_t)s->g_nodes.size() + 64u;
   kp.motion_uniform = s->motion_uniform ? 1u : 0u;
