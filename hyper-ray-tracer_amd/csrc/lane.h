@@ -81,6 +81,7 @@ struct Counts {
 
 struct TRay {
   Vec3 o, d, inv;
+  Vec3 minv; /* EXACT_MARGIN * |inv|: the inflated test's widening per unit of box distance */
   float time;
   float dd;  /* dot(d, d): sphere.rs:42 `a`, constant for the ray */
   float rdd; /* RN(1 / dd) for div_rn, or NaN when dd is outside div_rn's fast domain */
@@ -123,6 +124,7 @@ HRT_LANE_FI void set_dir(TRay& r, Vec3 o, Vec3 d) {
   r.d = d;
   /* aabb.rs:22 computes 1/d per call; the value is the same every time */
   r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  r.minv = v3(G::EXACT_MARGIN * fabsf(r.inv.x), G::EXACT_MARGIN * fabsf(r.inv.y), G::EXACT_MARGIN * fabsf(r.inv.z));
   r.dd = dot(d, d);
   r.rdd = div_rn_y(r.dd);
 }
@@ -267,17 +269,19 @@ HRT_LANE_FI bool box_infl(const float4& a, const float4& b, const TRay& r, float
   float dist = 0.0f;
 #pragma unroll
   for (int k = 0; k < 3; k++) dist = fmaxf(dist, fmaxf(fabsf(dmn[k]), fabsf(dmx[k])));
-  const float margin = G::EXACT_MARGIN * dist;
-  /* !(min(tmax, h0, h1, h2) < max(tmin, l0, l1, l2)) with NaN bounds ignored, i.e. no pair
+  /* widening dist * (EXACT_MARGIN |inv_k|), the per-ray factor precomputed (set_dir): it differs from
+   * (EXACT_MARGIN dist) |inv_k| by an ulp, far inside the 1.65x slack of EXACT_MARGIN.
+   * !(min(tmax, h0, h1, h2) < max(tmin, l0, l1, l2)) with NaN bounds ignored, i.e. no pair
    * (lower, upper) out of order, written as three comparisons: the widened bounds come from fmas
    * (canonical), so max3/min3 need no quieting, and tmin / tmax only meet comparisons (fmaxf/fminf on
    * them cost a canonicalising v_max per operand per node step).  The fourth pair, tmin <= tmax, holds
    * on every walk (tmax is +inf or an accepted root >= tmin). */
+  const float mi[3] = {r.minv.x, r.minv.y, r.minv.z};
   float l[3], h[3];
 #pragma unroll
   for (int k = 0; k < 3; k++) {
-    l[k] = fmaf(-margin, fabsf(inv[k]), ts[k]);
-    h[k] = fmaf(margin, fabsf(inv[k]), te[k]);
+    l[k] = fmaf(-dist, mi[k], ts[k]);
+    h[k] = fmaf(dist, mi[k], te[k]);
   }
   const float lo = fmaxf(fmaxf(l[0], l[1]), l[2]); /* NaN only if all three are: no constraint */
   const float hi = fminf(fminf(h[0], h[1]), h[2]);
@@ -858,12 +862,30 @@ HRT_LANE_FI bool walk_pending(uint32_t i) { return i - WALK_PEND < 0x7FFFFFFFu; 
 /* A BASIC scene holds K_BOX, K_BOX_PRIM and K_PRIM nodes only (F_BASIC: no instances or media), so
  * kp >= K_PRIM << 24 holds exactly for the nodes the inflated test must pass: K_PRIM (no box) and
  * NODE_REF_ONLY (bit 31). */
-template <int CULL, bool COUNT>
+/* STRIDE: the walk position is a node index (1), or the node's LDS byte address (32, sizeof(Node)):
+ * the LDS-resident stream is staged with its skip links turned into LDS addresses, so a step loads
+ * its node straight from the position, with no address arithmetic. */
+template <uint32_t STRIDE>
+HRT_LANE_FI void load_node(const G::Node* nodes, uint32_t i, float4& a, float4& b) {
+  static_assert(STRIDE == 1 || STRIDE == sizeof(G::Node), "node index or LDS byte address");
+  if constexpr (STRIDE == 1) {
+    a = ld4(nodes[i].mn);
+    b = ld4(nodes[i].mx);
+  } else {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef __attribute__((address_space(3))) const float4 lds_float4;
+    const lds_float4* p = (const lds_float4*)(size_t)i;
+    a = p[0];
+    b = p[1];
+#endif
+  }
+}
+
+template <int CULL, bool COUNT, uint32_t STRIDE = 1>
 HRT_LANE_FI void basic_box(const KParams& P, const G::Node* __restrict__ nodes, uint32_t& i, const TRay& r,
                            float closest, Counts& cn) {
-  const G::Node* np = nodes + i;
-  const float4 a = ld4(np->mn);
-  const float4 b = ld4(np->mx);
+  float4 a, b;
+  load_node<STRIDE>(nodes, i, a, b);
   uint32_t skip = f2u(a.w);
 #if defined(__HIP_DEVICE_COMPILE__)
   /* keep the skip link in the node's first 16-B load: left to itself the compiler narrows that load
@@ -878,20 +900,20 @@ HRT_LANE_FI void basic_box(const KParams& P, const G::Node* __restrict__ nodes, 
   else
     pass = box_hit<CULL>(a, b, r, P.t_min, closest) || ((kp >> 24) & G::KIND_MASK) == G::K_PRIM;
   const bool prim = (kp & (G::KIND_MASK << 24)) != 0u; /* K_BOX_PRIM or K_PRIM: a primitive to test */
-  const uint32_t next = i + (prim ? 1u + WALK_PEND : 1u);
+  const uint32_t next = i + (prim ? STRIDE + WALK_PEND : STRIDE);
   i = pass ? next : skip;
 }
 
 /* i = the walk position with WALK_PEND set; clears it and tests the leaf (i - 1)'s primitive */
-template <int CULL, bool COUNT>
+template <int CULL, bool COUNT, uint32_t STRIDE = 1>
 HRT_LANE_FI void basic_prim(const KParams& P, const G::Node* __restrict__ nodes, const G::Prim* __restrict__ prims,
                             uint32_t& i, const TRay& r, float& closest, uint32_t& winner, Counts& cn) {
   i -= WALK_PEND;
-  const G::Node* np = nodes + (i - 1u);
-  const float4 b = ld4(np->mx);
+  float4 a, b;
+  load_node<STRIDE>(nodes, i - STRIDE, a, b);
   const uint32_t kp = f2u(b.w);
   if constexpr (CULL == G::CULL_EXACT) {
-    if (((kp >> 24) & G::KIND_MASK) != G::K_PRIM && !box_ref(ld4(np->mn), b, r, P.t_min, closest)) return;
+    if (((kp >> 24) & G::KIND_MASK) != G::K_PRIM && !box_ref(a, b, r, P.t_min, closest)) return;
   }
   const uint32_t payload = kp & 0xFFFFFFu;
   const G::Prim* pp = prims + payload;

@@ -81,13 +81,21 @@ __global__ void debug_path_kernel(KParams P, uint32_t px, uint32_t py, uint32_t 
 template <bool LDS, bool FAST>
 constexpr int block_threads() { return LDS ? (FAST ? 1024 : 512) : 256; }
 
-/* Copy the node stream and primitive records into this workgroup's LDS. */
-__device__ __forceinline__ void stage_scene(const KParams& P, float4* lds, const G::Node*& nodes, const G::Prim*& prims) {
+/* Copy the node stream and primitive records into this workgroup's LDS.  BYTE_LINKS: store each skip
+ * link as the LDS byte address of its target (base + skip x sizeof(Node)), for walks whose position is
+ * that address (basic_box STRIDE 32). */
+template <bool BYTE_LINKS = false>
+__device__ __forceinline__ void stage_scene(const KParams& P, float4* lds, const G::Node*& nodes, const G::Prim*& prims,
+                                            uint32_t base = 0u) {
   const uint32_t n4 = P.n_nodes * (uint32_t)(sizeof(G::Node) / 16);
   const uint32_t p4 = P.n_prims * (uint32_t)(sizeof(G::Prim) / 16);
   const float4* gn = reinterpret_cast<const float4*>(P.nodes);
   const float4* gp = reinterpret_cast<const float4*>(P.prims);
-  for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) lds[k] = gn[k];
+  for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) {
+    float4 v = gn[k];
+    if (BYTE_LINKS && (k & 1u) == 0u) v.w = __uint_as_float(base + __float_as_uint(v.w) * (uint32_t)sizeof(G::Node));
+    lds[k] = v;
+  }
   for (uint32_t k = threadIdx.x; k < p4; k += blockDim.x) lds[n4 + k] = gp[k];
   __syncthreads();
   nodes = reinterpret_cast<const G::Node*>(lds);
@@ -270,11 +278,14 @@ void render_basic_kernel(KParams P) {
   extern __shared__ float4 lds_scene[];
   const G::Node* nodes = P.nodes;
   const G::Prim* prims = P.prims;
-  if constexpr (LDS) stage_scene(P, lds_scene, nodes, prims);
+  /* with the scene in LDS the walk position is the node's LDS byte address (basic_box STRIDE) */
+  constexpr uint32_t STRIDE = LDS ? (uint32_t)sizeof(G::Node) : 1u;
+  const uint32_t root = LDS ? (uint32_t)(size_t)(__attribute__((address_space(3))) float4*)lds_scene : 0u;
+  if constexpr (LDS) stage_scene<true>(P, lds_scene, nodes, prims, root);
   const uint32_t lane = threadIdx.x & 63u;
   const float scale = 1.0f / (float)P.spp; /* application.rs:403 */
   const float inf = __uint_as_float(0x7f800000u);
-  const uint32_t end = P.main_end;
+  const uint32_t end = root + P.main_end * STRIDE;
   const uint32_t need = P.postpone;
   const uint32_t batch = P.prim_batch;
   /* watchdog: a lane's walk is at most walk_cap steps; waiting for a batch can stretch a pass to the
@@ -313,7 +324,7 @@ void render_basic_kernel(KParams P) {
       set_ray(r, ps.ro, ps.rd, ps.rtime, P);
       closest = inf;
       winner = G::NONE;
-      node = ps.depth_left == 0 ? G::NONE : 0u; /* max_depth 0: black without a world.hit (:478-480) */
+      node = ps.depth_left == 0 ? G::NONE : root; /* max_depth 0: black without a world.hit (:478-480) */
     }
     /* step the walks until enough lanes have finished (lanes not walking hold node >= end).  A lane
      * whose leaf box passed holds WALK_PEND in `node` and waits; the wave runs the sphere block
@@ -327,13 +338,13 @@ void render_basic_kernel(KParams P) {
 #pragma unroll
       for (int u = 0; u < WALK_UNROLL; u++) {
         if constexpr (COUNT) cn.walk_slots++;
-        if (node < end) basic_box<CULL, COUNT>(P, nodes, node, r, closest, cn);
+        if (node < end) basic_box<CULL, COUNT, STRIDE>(P, nodes, node, r, closest, cn);
         if ((u + 1) % PRIM_EVERY != 0) continue;
         const bool waiting = walk_pending(node);
         const unsigned long long pm = __ballot(waiting);
         if (pm && ((uint32_t)__popcll(pm) >= batch || !__ballot(node < end))) {
           if constexpr (COUNT) cn.prim_slots++;
-          if (waiting) basic_prim<CULL, COUNT>(P, nodes, prims, node, r, closest, winner, cn);
+          if (waiting) basic_prim<CULL, COUNT, STRIDE>(P, nodes, prims, node, r, closest, winner, cn);
         }
       }
       const unsigned long long live = __ballot(node < end || walk_pending(node));
@@ -374,7 +385,7 @@ void render_basic_kernel(KParams P) {
         set_dir(r, ps.ro, ps.rd); /* the scattered ray keeps the sample's shutter time */
         closest = inf;
         winner = G::NONE;
-        node = 0u;
+        node = root;
       }
     }
     n_seg += (uint32_t)__popcll(__ballot(traced));
