@@ -49,6 +49,7 @@ struct KParams {
   float lens_radius, time0, time1;
   /* render */
   uint32_t W, H, spp, max_depth, sample_offset;
+  float rw1, rh1; /* RN(1 / (W - 1)), RN(1 / (H - 1)): set_pixel_rcp */
   float t_min;
   Vec3 background;
   uint64_t seed;
@@ -723,13 +724,26 @@ struct PathState {
 };
 
 /* application.rs:444-447 + camera.rs:85-95: jitter, lens sample, shutter time */
+/* host side: the reciprocals start_sample's camera divisions use (W, H >= 2) */
+inline void set_pixel_rcp(KParams& P) {
+  P.rw1 = 1.0f / ((float)P.W - 1.0f);
+  P.rh1 = 1.0f / ((float)P.H - 1.0f);
+}
+
 HRT_LANE_FI void start_sample(const KParams& P, PathState& ps, uint32_t px, uint32_t py,
                                              uint32_t sample) {
   ps.pk.pkey = path_key(P.seed, py * P.W + px, P.sample_offset + sample);
   ps.pk.segment = 0;
   ps.rng = rng_from_key(ps.pk.pkey);
-  float u = ((float)px + ps.rng.gen_f32()) / ((float)P.W - 1.0f);
-  float v = ((float)py + ps.rng.gen_f32()) / ((float)P.H - 1.0f);
+  /* application.rs:444-445 u, v: x / (W - 1) correctly rounded by div_rn's 3-instruction core with the
+   * host's RN(1 / (W - 1)).  Render parameters hold 2 <= W, H <= 65535 and x = px + gen_f32() is 0
+   * (exact: the core returns +0) or in [2^-24, 2^16], so a and q0 lie inside the proven domain
+   * (tests/native/div_rn_check.c) and the IEEE fallback is never needed. */
+  const float xu = (float)px + ps.rng.gen_f32(), aw = (float)P.W - 1.0f;
+  const float xv = (float)py + ps.rng.gen_f32(), ah = (float)P.H - 1.0f;
+  const float qu = xu * P.rw1, qv = xv * P.rh1;
+  float u = fmaf(fmaf(-qu, aw, xu), P.rw1, qu);
+  float v = fmaf(fmaf(-qv, ah, xv), P.rh1, qv);
   Vec3 disk = random_in_unit_disk(ps.rng);
   ps.rtime = ps.rng.gen_range_f32(P.time0, P.time1);
   Vec3 rdk = P.lens_radius * disk;

@@ -760,6 +760,7 @@ KParams scene_params(const hrt_scene* s, const hrt_camera* cam, const hrt_render
   kp.time1 = cam->time1;
   kp.W = p->width;
   kp.H = p->height;
+  set_pixel_rcp(kp);
   kp.spp = p->samples;
   kp.max_depth = p->max_depth;
   kp.sample_offset = p->sample_offset;

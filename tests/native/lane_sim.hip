@@ -128,6 +128,7 @@ int lane_sim_render(const void* blob, const hrt_blob_info* bi, const hrt_camera*
   P.time1 = cam->time1;
   P.W = p->width;
   P.H = p->height;
+  set_pixel_rcp(P);
   P.spp = p->samples;
   P.max_depth = p->max_depth;
   P.sample_offset = p->sample_offset;
