@@ -89,8 +89,8 @@ struct TRay {
   float tau; /* (time - time0) / (time1 - time0) of the scene's moving spheres (uniform motion only) */
 };
 
-/* x / r.dd correctly rounded (bit-identical to IEEE division) in 3 instructions instead of the
- * ~11 of the general sequence: with y = RN(1/a), q0 = RN(x*y) is within one ulp of x/a, the
+/* x / r.dd correctly rounded (bit-identical to IEEE division) by a 3-instruction core: with
+ * y = RN(1/a), q0 = RN(x*y) is within one ulp of x/a, the
  * residual x - q0*a is exact in an fma, and RN(q0 + residual*y) is RN(x/a) (Markstein's theorem;
  * no under/overflow anywhere while |x|, |q0|, a lie in [2^-100, 2^100]).  Zero, NaN, inf and
  * extreme exponents take the IEEE sequence.  tests/test_fast_division.py checks 6e7 cases on the host
@@ -98,8 +98,10 @@ struct TRay {
  * The domain test is split so that one check per call remains: the per-ray y is NaN unless
  * a in [2^-49, 2^49] (div_rn_y), and the call checks |q0| in [2^-50, 2^50].  Together they imply
  * |x| = |q0 a| (1 +- 2^-23) in [2^-100, 2^100], so this domain lies inside the one above; a NaN y
- * fails the |q0| check.  The IEEE sequence sits behind a wave vote: if-converted, every call would
- * pay for both sequences. */
+ * fails the |q0| check.  Default build (HRT_DIV_VOTE 0): the IEEE fallback is if-converted, so a call
+ * executes the core AND the ~11-instruction IEEE sequence and selects (measured cheaper than a
+ * branch); HRT_DIV_VOTE 1 puts the fallback behind a wave vote instead.  Only the camera divisions
+ * (start_sample) run the bare 3-instruction core, with no fallback. */
 HRT_LANE_FI float div_rn_y(float a) { return a >= 0x1p-49f && a <= 0x1p49f ? 1.0f / a : u2f(0x7fc00000u); }
 HRT_LANE_FI float div_rn(float x, float a, float y) {
   const float q0 = x * y;
@@ -736,9 +738,17 @@ HRT_LANE_FI void start_sample(const KParams& P, PathState& ps, uint32_t px, uint
   ps.pk.segment = 0;
   ps.rng = rng_from_key(ps.pk.pkey);
   /* application.rs:444-445 u, v: x / (W - 1) correctly rounded by div_rn's 3-instruction core with the
-   * host's RN(1 / (W - 1)).  Render parameters hold 2 <= W, H <= 65535 and x = px + gen_f32() is 0
-   * (exact: the core returns +0) or in [2^-24, 2^16], so a and q0 lie inside the proven domain
-   * (tests/native/div_rn_check.c) and the IEEE fallback is never needed. */
+   * host's y = RN(1 / a), a = W - 1, and no IEEE fallback.  Why that is exact here (render parameters
+   * hold 2 <= W, H <= 65535, so a is an integer in [1, 65534]; x = RN(px + gen_f32()) is 0 or an f32
+   * multiple of 2^-24 in [2^-24, 2^16]):
+   *  - x = 0 gives q0 = 0 and the core returns +0, as IEEE does;
+   *  - q0 = RN(x y) is within 1.5 ulp of x / a, so the residual fma(-q0, a, x) is exact and
+   *    q0 + r y = x / a + r (y - 1/a) with |r (y - 1/a)| <= a ulp 2^-24 / a = 2^-24 ulp of the quotient;
+   *  - x / a = N 2^-24 / a with N integer, so its distance to any rounding midpoint (2j+1) 2^(e-24) is
+   *    0 or >= 2^-24 2^min(e,0) / a >= 2^-17 ulp, far above the 2^-24 ulp perturbation;
+   *  - it is never 0: x = a m would need the >= 25 odd significant bits of m (times a) in an f32.
+   * So the final RN lands on RN(x / a).  tests/native/div_rn_check.c `camera` checks every a in
+   * [1, 65534] at the edge values of x (tests/test_fast_division.py). */
   const float xu = (float)px + ps.rng.gen_f32(), aw = (float)P.W - 1.0f;
   const float xv = (float)py + ps.rng.gen_f32(), ah = (float)P.H - 1.0f;
   const float qu = xu * P.rw1, qv = xv * P.rh1;

@@ -589,6 +589,28 @@ hrt_status hguard(F&& f) {
 
 constexpr size_t SLOT_HDR = 128; /* work counter + 12 stats words + error word, padded */
 
+constexpr const char* SLOT_ERROR_MSG =
+    "a render launch on this scene stopped walks that did not terminate (corrupt scene data); its frame is incomplete";
+
+/* Render parameters every kernel entry point accepts: 2 <= W, H <= 65535 (start_sample's camera
+ * divisions use host reciprocals proven exact there, lane.h), spp > 0, known flags, a shutter interval. */
+void check_render_args(const hrt_camera* cam, const hrt_render_params* p) {
+  if (p->width < 2 || p->height < 2 || p->width > 65535 || p->height > 65535 || p->samples == 0 ||
+      (p->flags & ~(uint32_t)(HRT_RENDER_COUNT_WORK | HRT_RENDER_NO_LDS | HRT_RENDER_REFERENCE_CULL |
+                              HRT_RENDER_FAST_CULL | HRT_RENDER_SAH)) != 0)
+    throw HipError{HRT_ERR_INVALID_ARG, "bad render params (2 <= width, height <= 65535, samples > 0, known flags)"};
+  if (!(cam->time0 < cam->time1)) throw HipError{HRT_ERR_INVALID_ARG, "camera time0 must be < time1"};
+}
+
+/* The watchdog's error word of a slot's finished launch (pinned copy, word 12): report it once. */
+void take_slot_error(hrt_scene::Slot& sl) {
+  unsigned long long* h = (unsigned long long*)sl.h_tiles;
+  if (h && h[12] != 0) {
+    h[12] = 0;
+    throw HipError{HRT_ERR_STATE, SLOT_ERROR_MSG};
+  }
+}
+
 
 /* persistent grid: as many workgroups as are co-resident on the device (cached per kernel/device) */
 int resident_grid(const void* fn, int block, int device, size_t smem, bool lds) {
@@ -840,10 +862,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     if (!s || !cam || !p || !tiles || !d_rgba || n_tiles == 0)
       throw HipError{HRT_ERR_INVALID_ARG, "hrt_render_tiles_device: null argument"};
     if (!s->committed || !s->d_blob) throw HipError{HRT_ERR_STATE, "scene not committed"};
-    if (p->width < 2 || p->height < 2 || p->width > 65535 || p->height > 65535 || p->samples == 0 || (p->flags & ~(uint32_t)(HRT_RENDER_COUNT_WORK | HRT_RENDER_NO_LDS | HRT_RENDER_REFERENCE_CULL |
-                                     HRT_RENDER_FAST_CULL | HRT_RENDER_SAH)) != 0)
-      throw HipError{HRT_ERR_INVALID_ARG, "bad render params (width/height >= 2, samples > 0, known flags)"};
-    if (!(cam->time0 < cam->time1)) throw HipError{HRT_ERR_INVALID_ARG, "camera time0 must be < time1"};
+    check_render_args(cam, p);
     /* sample chunks: spp <= 32 keeps one work item per pixel (the reference's sequential sum);
      * larger spp splits into <= 16 chunks so the frame's tail is a chunk, not a whole pixel */
     const uint32_t spp = p->samples;
@@ -865,8 +884,15 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     DeviceGuard dg(s->device);
     /* scratch slot: device [counter u32 | pad | stats 8 x u64 | pad to HDR | tiles], pinned host [stats | tiles] */
     std::lock_guard<std::mutex> lock(*static_cast<std::mutex*>(s->slot_mutex));
+    /* an earlier launch whose walks the watchdog killed is reported by the first call that sees its
+     * copied-back error word (every launch copies it, with or without stats) */
+    for (auto& other : s->slots)
+      if (other.used && hipEventQuery((hipEvent_t)other.event) == hipSuccess) take_slot_error(other);
     hrt_scene::Slot& sl = s->slots[s->next_slot++ % hrt_scene::N_SLOTS];
-    if (sl.used) hip_check(hipEventSynchronize((hipEvent_t)sl.event), "hipEventSynchronize(slot)");
+    if (sl.used) {
+      hip_check(hipEventSynchronize((hipEvent_t)sl.event), "hipEventSynchronize(slot)");
+      take_slot_error(sl);
+    }
     size_t tiles_bytes = n_tiles * sizeof(G::TileDev);
     if (tiles_bytes > sl.tiles_cap) {
       if (sl.d_mem) hip_check(hipFree(sl.d_mem), "hipFree(slot)");
@@ -911,12 +937,15 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
                          (float4*)d_rgba, (uint32_t)outp, n_chunks, spp);
       hip_check(hipGetLastError(), "reduce_chunks launch");
     }
+    /* the stats words and the watchdog's error word (h[12]) come back after EVERY launch, so a killed
+     * frame is reported even when the caller asked for no stats (take_slot_error) */
     unsigned long long* h = (unsigned long long*)sl.h_tiles;
-    if (stats) hip_check(hipMemcpyAsync(h, (uint8_t*)scratch + 8, 104, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(stats)");
+    hip_check(hipMemcpyAsync(h, (uint8_t*)scratch + 8, 104, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(stats)");
     hip_check(hipEventRecord((hipEvent_t)sl.event, stream), "hipEventRecord(slot)");
     sl.used = true;
     if (stats) {
       hip_check(hipEventSynchronize((hipEvent_t)sl.event), "hipEventSynchronize(stats)");
+      take_slot_error(sl);
       stats->segments = h[0];
       stats->samples = h[1];
       stats->pixels = h[2];
@@ -927,8 +956,39 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
       stats->shade_slots = h[7];
       stats->prim_slots = h[8];
       for (int k = 0; k < 3; k++) stats->phase_cycles[k] = h[9 + k];
-      if (h[12] != 0) throw HipError{HRT_ERR_STATE, "a walk did not terminate (corrupt scene data); frame incomplete"};
     }
+  });
+}
+
+hrt_status hrt_scene_synchronize(hrt_scene* s) {
+  return hguard([&] {
+    if (!s) throw HipError{HRT_ERR_INVALID_ARG, "hrt_scene_synchronize: null scene"};
+    if (!s->committed || !s->slot_mutex) return;
+    DeviceGuard dg(s->device);
+    std::lock_guard<std::mutex> lock(*static_cast<std::mutex*>(s->slot_mutex));
+    bool failed = false;
+    for (auto& sl : s->slots) {
+      if (!sl.used) continue;
+      hip_check(hipEventSynchronize((hipEvent_t)sl.event), "hipEventSynchronize(slot)");
+      try {
+        take_slot_error(sl);
+      } catch (const HipError&) {
+        failed = true; /* keep draining the other slots, report once */
+      }
+    }
+    if (failed) throw HipError{HRT_ERR_STATE, SLOT_ERROR_MSG};
+  });
+}
+
+hrt_status hrt_debug_poke_blob(hrt_scene* s, uint64_t offset, const void* data, uint64_t n) {
+  return hguard([&] {
+    if (!s || !data) throw HipError{HRT_ERR_INVALID_ARG, "hrt_debug_poke_blob: null argument"};
+    if (!s->committed || !s->d_blob) throw HipError{HRT_ERR_STATE, "scene not committed"};
+    if (offset > s->blob_bytes || n > s->blob_bytes - offset)
+      throw HipError{HRT_ERR_INVALID_ARG, "hrt_debug_poke_blob: range outside the scene blob"};
+    DeviceGuard dg(s->device);
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    hip_check(hipMemcpy((uint8_t*)s->d_blob + offset, data, n, hipMemcpyHostToDevice), "hipMemcpy(poke)");
   });
 }
 
@@ -1063,6 +1123,7 @@ hrt_status hrt_debug_trace_path(hrt_scene* s, const hrt_camera* cam, const hrt_r
     if (!s || !cam || !p || !out || !n_segments || max_segments == 0)
       throw HipError{HRT_ERR_INVALID_ARG, "hrt_debug_trace_path: bad argument"};
     if (!s->committed || !s->d_blob) throw HipError{HRT_ERR_STATE, "scene not committed"};
+    check_render_args(cam, p);
     if (x >= p->width || y >= p->height) throw HipError{HRT_ERR_INVALID_ARG, "pixel outside the image"};
     DeviceGuard dg(s->device);
     const Plan pl = plan(s, cam, p->flags);

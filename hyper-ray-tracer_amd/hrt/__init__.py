@@ -136,6 +136,7 @@ EXPORTS = [
     "hrt_node_bounding_box", "hrt_scene_set_root", "hrt_scene_commit", "hrt_preset_build", "hrt_camera_init",
     "hrt_render_tiles_device", "hrt_render_device", "hrt_render", "hrt_tile_grid", "hrt_scene_get_info",
     "hrt_debug_device_math", "hrt_debug_trace_path", "hrt_debug_scene_blob", "hrt_image_write", "hrt_render_progressive", "hrt_debug_prim_record",
+    "hrt_scene_synchronize", "hrt_debug_poke_blob",
 ]
 
 _lib = None
@@ -203,6 +204,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hrt_render_progressive": (S, [vp, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), u32, u32, u32, u32,
                                        TILE_FN, vp, ctypes.POINTER(RenderStats)]),
         "hrt_debug_trace_path": (S, [vp, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), u32, u32, u32, u32, vp, _U32P]),
+        "hrt_scene_synchronize": (S, [vp]),
+        "hrt_debug_poke_blob": (S, [vp, u64, vp, u64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -331,6 +334,16 @@ class Scene:
 
     def commit(self, device: int = -1):
         _check(load().hrt_scene_commit(self.h, device))
+
+    def synchronize(self):
+        """Wait for every render launched on this scene; raises HrtError(ERR_STATE) if one of them
+        was stopped by the walk watchdog (hrt_scene_synchronize)."""
+        _check(load().hrt_scene_synchronize(self.h))
+
+    def poke_blob(self, offset: int, data: bytes):
+        """Fault injection: overwrite bytes of the committed device blob (hrt_debug_poke_blob)."""
+        buf = ctypes.create_string_buffer(bytes(data), len(data))
+        _check(load().hrt_debug_poke_blob(self.h, offset, buf, len(data)))
 
     def scene_info(self) -> SceneInfo:
         si = SceneInfo()

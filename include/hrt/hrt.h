@@ -67,7 +67,9 @@ typedef struct hrt_camera {
  * hard-codes (background per scene application.rs:132-197, t_min = 0.001 at :482) + the seed that
  * replaces thread_rng.  Pixels are keyed by their index in the FULL width x height image. */
 typedef struct hrt_render_params {
-  uint32_t width, height;   /* full image (u = (x+xi)/(width-1), application.rs:444) */
+  uint32_t width, height;   /* full image (u = (x+xi)/(width-1), application.rs:444); each must lie in
+                               [2, 65535] (HRT_ERR_INVALID_ARG otherwise): the camera divisions are
+                               computed with host reciprocals proven exact on that range only */
   uint32_t samples;         /* spp (application.rs:443) */
   uint32_t max_depth;       /* ray_color depth (application.rs:478); reference CLI default 10 */
   uint32_t sample_offset;   /* first sample index (0; >0 splits one pixel's samples across jobs) */
@@ -213,10 +215,17 @@ hrt_status hrt_camera_init(hrt_camera* cam, const float look_from[3], const floa
 /* Render `n_tiles` tiles into device memory d_rgba (tiles packed back to back, tile i at
  * 4 * sum_{j<i} w_j*h_j floats; each tile row-major with y up).  Asynchronous on `stream`
  * (a hipStream_t, NULL = default stream).  stats (optional, host pointer) is filled after an
- * internal stream synchronisation when non-NULL. */
+ * internal stream synchronisation when non-NULL.
+ * Errors of the launch itself: with stats, HRT_ERR_STATE when the walk watchdog stopped walks that
+ * could not end (corrupt scene data; the frame is incomplete).  Without stats the call returns before
+ * the kernel ends; such a launch is then reported as HRT_ERR_STATE by the first later call on the
+ * scene that finds it finished (the next hrt_render_* call, or hrt_scene_synchronize). */
 hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hrt_render_params* p,
                                    const hrt_tile* tiles, uint32_t n_tiles, float* d_rgba,
                                    void* stream, hrt_render_stats* stats);
+/* Wait for every render launched on the scene; HRT_ERR_STATE if one of them did not complete its
+ * frame (walk watchdog) and no earlier call has reported it. */
+hrt_status hrt_scene_synchronize(hrt_scene* s);
 /* One delivered tile (application.rs:45-52 Tile): tile-grid indices (pixel origin = index * tile_size),
  * size in pixels, and RGBA f32 pixels row-major in the tile (row 0 = bottom).  `pixels` is valid only
  * during the callback. */
@@ -257,8 +266,6 @@ typedef struct hrt_scene_info {
   uint32_t sah_stream_len; /* >0: sphere-only scene with the SAH octant streams (8 x this many nodes) */
 } hrt_scene_info;
 hrt_status hrt_scene_get_info(const hrt_scene* s, hrt_scene_info* info);
-/* Evaluate the shared deterministic math on the DEVICE (op: 0 sin,1 cos,2 acos,3 atan2,4 ln,
- * 5 pow5, 6 tan) for n inputs; used by the GPU KAT test to prove host/device bit identity. */
 /* Write an RGBA f32 frame (w x h, row-major, row 0 = image y 0 = bottom, as the render calls produce;
  * alpha is dropped) to `path` in an HRT_IMAGE_* format. */
 hrt_status hrt_image_write(const char* path, const float* rgba, uint32_t w, uint32_t h, int32_t format);
@@ -286,8 +293,14 @@ typedef struct hrt_blob_info {
   float box_t0, box_t1;    /* ray times the BVH boxes are valid for */
 } hrt_blob_info;
 hrt_status hrt_debug_scene_blob(hrt_scene* s, void* out, uint64_t cap, uint64_t* size, hrt_blob_info* info);
+/* Overwrite n bytes of the committed scene's DEVICE blob at byte `offset` (hrt_blob_info offsets), after
+ * a device synchronisation.  Fault injection for the watchdog test (e.g. a skip link pointing back). */
+hrt_status hrt_debug_poke_blob(hrt_scene* s, uint64_t offset, const void* data, uint64_t n);
 /* The flattened 48-byte record of a primitive (order 0: reference pre-order, 1: SAH streams). */
 hrt_status hrt_debug_prim_record(const hrt_scene* s, int32_t order, uint32_t index, float* out12);
+/* Evaluate the shared deterministic math on the DEVICE (op: 0 sin, 1 cos, 2 acos, 3 atan2, 4 ln,
+ * 5 pow5, 6 tan, 7 the walk's division x / y) for n inputs; used by the GPU KAT test to prove
+ * host/device bit identity. */
 hrt_status hrt_debug_device_math(int32_t op, const float* x, const float* y, float* out, uint32_t n);
 
 #ifdef __cplusplus

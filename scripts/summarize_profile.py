@@ -1,72 +1,134 @@
 """Summarise rocprofv3 outputs (kernel stats + FETCH/WRITE/SQ PMC passes) of one bench run.
 
   python scripts/summarize_profile.py <tag> <preset> <W> <H> <spp>
-Reads gpurun_out/prof_<tag>_{kt,fetch,write,sq}/, writes profiles/<tag>_summary.md (+ the raw
-kernel_stats csv) and updates profiles/pmc_traffic.json (HBM bytes per launch of the render kernel,
-FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 note; bench.py reports it as roofline.traffic).
+Reads gpurun_out/prof_<tag>_{kt,fetch,write,sq,sq2}/ (scripts/profile.sh), writes
+profiles/<tag>_summary.md (+ the raw kernel_stats csv) and updates profiles/roofline_pmc.json, which
+bench.py reads for its `roofline` object:
+  - valu_insts  : SQ_INSTS_VALU of one render launch (wave-instructions, all SIMDs);
+  - clock_hz    : GRBM_GUI_ACTIVE / 8 XCDs / kernel time (MI355X_MICROARCH.md, DVFS give-back);
+  - hbm_bytes   : 2 x FETCH_SIZE + WRITE_SIZE (FETCH_SIZE doubled per the gfx950 note of the guide);
+  - lds_*       : SQ_INSTS_LDS, SQ_LDS_BANK_CONFLICT, SQ_LDS_IDX_ACTIVE;
+  - lib_sha16   : which libhrt.so build the counters belong to (bench reports whether it matches).
+The launch profiled is the first timed-kernel dispatch of the run (the warm-up frame with stats).
 """
 import csv
+import hashlib
 import json
 import os
 import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-tag, preset, W, H, spp = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4], sys.argv[5]
-src = os.path.join(ROOT, "gpurun_out")
-dst = os.path.join(ROOT, "profiles")
-os.makedirs(dst, exist_ok=True)
+SIMDS = 256 * 4
 
 
-def rows(name):
-    p = os.path.join(src, f"prof_{tag}_{name}", "run_counter_collection.csv")
-    return list(csv.DictReader(open(p))) if os.path.exists(p) else []
+def lib_sha16():
+    p = os.path.join(ROOT, "hyper-ray-tracer_amd", "lib", "libhrt.so")
+    return hashlib.sha256(open(p, "rb").read()).hexdigest()[:16] if os.path.exists(p) else None
 
 
-def per_dispatch(rs):
-    out = {}
-    for r in rs:
-        k = (int(r["Dispatch_Id"]), r["Kernel_Name"])
-        out.setdefault(k, {})
-        out[k][r["Counter_Name"]] = out[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-    return out
+def main():
+    tag, preset, W, H, spp = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
+    src = os.path.join(ROOT, "gpurun_out")
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+
+    def per_dispatch(name):
+        p = os.path.join(src, f"prof_{tag}_{name}", "run_counter_collection.csv")
+        out = {}
+        if not os.path.exists(p):
+            return out
+        for r in csv.DictReader(open(p)):
+            k = (int(r["Dispatch_Id"]), r["Kernel_Name"])
+            out.setdefault(k, {})
+            out[k][r["Counter_Name"]] = out[k].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        return out
+
+    def first_render(d):
+        """fallback without a kernel trace: the run's first render dispatch (bench's warm-up frame)"""
+        for (disp, name), v in sorted(d.items()):
+            if "render" in name and "reduce" not in name:
+                return name, v
+        return None, {}
+
+    lines = [f"# rocprofv3 summary `{tag}`: bench.py, {preset} {W}x{H} {spp} spp\n"]
+    kt = os.path.join(src, f"prof_{tag}_kt", "run_kernel_stats.csv")
+    kern_ms = None
+    kname = None
+    if os.path.exists(kt):
+        shutil.copy(kt, os.path.join(dst, f"{tag}_kernel_stats.csv"))
+        lines.append("## kernel stats (`--kernel-trace --stats`)\n\n| kernel | calls | avg ms | total ms |\n|---|---|---|---|")
+        rows = list(csv.DictReader(open(kt)))
+        for r in rows:
+            lines.append(f"| `{r['Name'][:100]}` | {r['Calls']} | {float(r['AverageNs'])/1e6:.3f} | {float(r['TotalDurationNs'])/1e6:.3f} |")
+        # the timed kernel: the most-called render instantiation (the COUNT twin runs once)
+        rk = [r for r in rows if "render" in r["Name"] and "reduce" not in r["Name"]]
+        if rk:
+            best = max(rk, key=lambda r: (int(r["Calls"]), -float(r["AverageNs"])))
+            kern_ms, kname = float(best["AverageNs"]) / 1e6, best["Name"]
+    sq, sq2 = per_dispatch("sq"), per_dispatch("sq2")
+    fetch, write = per_dispatch("fetch"), per_dispatch("write")
+
+    def timed(d):
+        if kname is None:
+            return first_render(d)[1]
+        short = kname.split("(")[0]
+        for (disp, name), v in sorted(d.items()):
+            if name.split("(")[0] == short:
+                return v
+        return {}
+
+    s1, s2, f, w = timed(sq), timed(sq2), timed(fetch), timed(write)
+    c = {**s1, **s2}
+    res = {"source": f"profiles/{tag}_summary.md", "kernel": kname, "kernel_avg_ms": kern_ms,
+           "lib_sha16": None if "--no-sha" in sys.argv else lib_sha16()}
+    if f and w:
+        res["hbm_bytes"] = int(2 * f.get("FETCH_SIZE", 0) * 1024 + w.get("WRITE_SIZE", 0) * 1024)
+        res["fetch_bytes_x2"] = int(2 * f.get("FETCH_SIZE", 0) * 1024)
+        res["write_bytes"] = int(w.get("WRITE_SIZE", 0) * 1024)
+        lines.append(f"\n## HBM traffic per launch (PMC, separate passes)\n\nFETCH_SIZE {f.get('FETCH_SIZE', 0):.0f} KB (x2 gfx950 "
+                     f"correction), WRITE_SIZE {w.get('WRITE_SIZE', 0):.0f} KB -> **{res['hbm_bytes']/1e9:.3f} GB per launch**"
+                     + (f" = {res['hbm_bytes']/1e9/(kern_ms*1e-3):.1f} GB/s over the kernel" if kern_ms else "") + "\n")
+    if c:
+        lines.append("## SQ / GRBM counters (one timed-kernel launch)\n")
+        for k in sorted(c):
+            lines.append(f"- {k}: {c[k]:.4g}")
+        g = c.get("GRBM_GUI_ACTIVE")
+        iv = c.get("SQ_INSTS_VALU")
+        if g and kern_ms:
+            cyc = g / 8.0  # per XCD
+            res["clock_hz"] = cyc / (kern_ms * 1e-3)
+            res["cycles_per_xcd"] = cyc
+        if iv:
+            res["valu_insts"] = iv
+        for k in ("SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_INSTS_SALU", "SQ_WAVES", "SQ_WAVE_CYCLES",
+                  "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_INSTS_VMEM"):
+            if k in c:
+                res[k.lower()] = c[k]
+        if g and iv:
+            frac = iv * 2.0 / (SIMDS * g / 8.0)
+            res["valu_issue_frac_measured_clock"] = frac
+            lines.append(f"\n**VALU issue**: {iv:.4g} wave-instructions x 2 cycles (wave64 on SIMD32) / (1024 SIMDs x {g/8:.4g} "
+                         f"cycles per XCD) = **{frac:.3f}** of issue capacity at the measured clock "
+                         f"({res.get('clock_hz', 0)/1e9:.2f} GHz)")
+            if "SQ_LDS_IDX_ACTIVE" in c:
+                lines.append(f"\n**LDS**: {c['SQ_INSTS_LDS']:.4g} LDS instructions, bank-conflict cycles "
+                             f"{c['SQ_LDS_BANK_CONFLICT']/c['SQ_LDS_IDX_ACTIVE']*100:.1f}% of {c['SQ_LDS_IDX_ACTIVE']:.4g} "
+                             f"LDS-array cycles = {c['SQ_LDS_IDX_ACTIVE']/256/(g/8)*100:.1f}% of each CU's cycles")
+            if "SQ_WAVE_CYCLES" in c and "SQ_WAIT_INST_ANY" in c:
+                wc = c["SQ_WAVE_CYCLES"]
+                lines.append(f"\n**Wave time**: issuing {c['SQ_ACTIVE_INST_ANY']/wc*100:.1f}%, waiting to issue (pipe busy / "
+                             f"dependency) {c['SQ_WAIT_INST_ANY']/wc*100:.1f}%, waiting on s_waitcnt {c['SQ_WAIT_ANY']/wc*100:.1f}%")
+    with open(os.path.join(dst, f"{tag}_summary.md"), "w") as fh:
+        fh.write("\n".join(lines) + "\n")
+    pj = os.path.join(dst, "roofline_pmc.json")
+    d = json.load(open(pj)) if os.path.exists(pj) else {}
+    d[f"{preset}_{W}x{H}_{spp}"] = res
+    with open(pj, "w") as fh:
+        json.dump(d, fh, indent=1)
+    print("\n".join(lines))
+    print(json.dumps(res, indent=1))
 
 
-def is_render(name):
-    return "render_kernel" in name or "render_basic_kernel" in name
-
-
-lines = [f"# rocprofv3 summary `{tag}`: bench.py, {preset} {W}x{H} {spp} spp\n"]
-kt = os.path.join(src, f"prof_{tag}_kt", "run_kernel_stats.csv")
-if os.path.exists(kt):
-    shutil.copy(kt, os.path.join(dst, f"{tag}_kernel_stats.csv"))
-    lines.append("## kernel stats (`--kernel-trace --stats`)\n\n| kernel | calls | avg ms | total ms |\n|---|---|---|---|")
-    for r in csv.DictReader(open(kt)):
-        lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs'])/1e6:.3f} | {float(r['TotalDurationNs'])/1e6:.3f} |")
-fetch, write, sq = per_dispatch(rows("fetch")), per_dispatch(rows("write")), per_dispatch(rows("sq"))
-main_f = [v for (d, n), v in sorted(fetch.items()) if is_render(n)]
-main_w = [v for (d, n), v in sorted(write.items()) if is_render(n)]
-main_sq = [(n, v) for (d, n), v in sorted(sq.items()) if is_render(n)]
-traffic = None
-if main_f and main_w:
-    # the first render dispatch of the run is the timed kernel's twin (stats warm-up)
-    f_kb, w_kb = main_f[0].get("FETCH_SIZE", 0.0), main_w[0].get("WRITE_SIZE", 0.0)
-    traffic = int(2 * f_kb * 1024 + w_kb * 1024)
-    lines.append(f"\n## HBM traffic per launch (PMC, separate passes)\n\nFETCH_SIZE {f_kb:.0f} KB (x2 gfx950 correction), "
-                 f"WRITE_SIZE {w_kb:.0f} KB -> **{traffic/1e9:.3f} GB per launch**\n")
-if main_sq:
-    n, v = main_sq[0]
-    waves = v.get("SQ_WAVES", 0)
-    lines.append("## SQ counters (first render dispatch)\n")
-    for k in sorted(v):
-        lines.append(f"- {k}: {v[k]:.4g}")
-    if v.get("GRBM_GUI_ACTIVE") and v.get("SQ_INSTS_VALU"):
-        lines.append(f"- VALU instructions per wave: {v['SQ_INSTS_VALU']/max(1,waves):.4g}")
-with open(os.path.join(dst, f"{tag}_summary.md"), "w") as fh:
-    fh.write("\n".join(lines) + "\n")
-pj = os.path.join(dst, "pmc_traffic.json")
-d = json.load(open(pj)) if os.path.exists(pj) else {}
-if traffic is not None:
-    d[f"{preset}_{W}x{H}_{spp}"] = {"hbm_bytes_per_launch": traffic, "source": f"profiles/{tag}_summary.md"}
-    json.dump(d, open(pj, "w"), indent=1)
-print("\n".join(lines))
+if __name__ == "__main__":
+    main()

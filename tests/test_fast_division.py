@@ -27,6 +27,16 @@ def test_fma_corrected_division_is_correctly_rounded(checker, seed, emin, emax):
     assert bad == 0
 
 
+def test_camera_divisions_exact_on_the_whole_parameter_range(checker):
+    """start_sample's u = x / (W - 1), v = y / (H - 1) use div_rn's bare core with host reciprocals and no
+    IEEE fallback (lane.h): every divisor W - 1 in [1, 65534] (the accepted 2 <= W <= 65535), x = px + a
+    gen_f32 draw at its edges (0, 2^-24, 0.5, 1 - 2^-24) and random, px in [0, W - 1]."""
+    out = subprocess.run([checker, "camera", "5"], check=True, capture_output=True, text=True).stdout.split()
+    cases, bad = int(out[0]), int(out[1])
+    assert cases == 65534 * 64
+    assert bad == 0
+
+
 def _pairs(n, rng):
     a = (rng.random(n, dtype=np.float32) * 8).astype(np.float32) * np.float32(2.0) ** rng.integers(-40, 40, n).astype(np.float32)
     x = (rng.standard_normal(n).astype(np.float32)) * np.float32(2.0) ** rng.integers(-40, 40, n).astype(np.float32)

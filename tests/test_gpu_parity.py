@@ -239,3 +239,66 @@ def test_progressive_tiles_assemble_the_frame(earth, batch, world):
         assert st.samples == sum(t[2] * t[3] for t in hrt.tile_grid(W, H, T, rank, world)) * 8
     assert len(seen) == len(set(seen)) == len(hrt.tile_grid(W, H, T))
     assert np.array_equal(frame, full)
+
+
+@pytest.mark.gpu
+def test_watchdog_reports_a_killed_frame_without_stats(earth):
+    """A corrupt skip link (a box node's fail link pointing back to the root) makes walks loop; the
+    watchdog stops them, and the frame is reported HRT_ERR_STATE although the launch asked for no stats:
+    by hrt_scene_synchronize, and by the call that next reuses the launch's scratch slot."""
+    import struct
+
+    import torch
+
+    s = hrt.preset("random", 1, earth)
+    s.commit()
+    _, info = hrt.scene_blob(s)
+    W, H = 64, 36
+    cam = hrt.preset_camera(s.info, W, H)
+    p = hrt.params(W, H, 2, 50, 3, tuple(s.info.background))
+    ok, st = hrt.render(s, cam, p, stats=True)  # intact scene first
+    assert st.pixels == W * H
+    # node 1 is the root's left child (a box node: pre-order); its skip link (dword 3) -> node 0
+    s.poke_blob(info.off_nodes + 32 * 1 + 12, struct.pack("<I", 0))
+    d = torch.zeros(W * H * 4, device="cuda")
+    hrt.render_tiles_device(s, cam, p, [(0, 0, W, H)], d.data_ptr(), 0)  # no stats: returns at once
+    with pytest.raises(hrt.HrtError) as e:
+        s.synchronize()
+    assert e.value.status == hrt.ERR_STATE and "did not terminate" in str(e.value)
+    s.synchronize()  # reported once
+    for _ in range(4):  # fill the slots; the 5th call reuses the first slot and finds its error
+        try:
+            hrt.render_tiles_device(s, cam, p, [(0, 0, W, H)], d.data_ptr(), 0)
+        except hrt.HrtError as err:
+            assert err.status == hrt.ERR_STATE
+            break
+    else:
+        with pytest.raises(hrt.HrtError) as e:
+            hrt.render_tiles_device(s, cam, p, [(0, 0, W, H)], d.data_ptr(), 0)
+        assert e.value.status == hrt.ERR_STATE
+    with pytest.raises(hrt.HrtError) as e:  # a synchronous call reports its own launch
+        hrt.render(s, cam, p)
+    assert e.value.status == hrt.ERR_STATE
+
+
+@pytest.mark.gpu
+def test_image_size_range_is_enforced(earth):
+    """2 <= width, height <= 65535 (the camera divisions' proven domain, lane.h start_sample)."""
+    s = hrt.preset("random", 1, earth)
+    s.commit()
+    for W, H in [(1, 8), (8, 1), (65536, 8), (8, 65536)]:
+        cam = hrt.preset_camera(s.info, max(W, 2), max(H, 2))
+        with pytest.raises(hrt.HrtError) as e:
+            hrt.render(s, cam, hrt.params(W, H, 1, 4, 1), region=(0, 0, 1, 1))
+        assert e.value.status == hrt.ERR_INVALID_ARG
+        with pytest.raises(hrt.HrtError) as e:
+            hrt.trace_path(s, cam, hrt.params(W, H, 1, 4, 1), 0, 0, 0)
+        assert e.value.status == hrt.ERR_INVALID_ARG
+    cam = hrt.preset_camera(s.info, 2, 2)
+    img = hrt.render(s, cam, hrt.params(2, 2, 2, 4, 1, tuple(s.info.background)))
+    ref, _ = O.OracleScene(0, 1, earth).render(2, 2, 2, 4, seed=1)
+    assert np.abs(img - ref).max() <= TOL
+    cam = hrt.preset_camera(s.info, 65535, 2)
+    img = hrt.render(s, cam, hrt.params(65535, 2, 1, 4, 1, tuple(s.info.background)), region=(65000, 0, 16, 2))
+    ref, _ = O.OracleScene(0, 1, earth).render(65535, 2, 1, 4, seed=1, region=(65000, 0, 16, 2))
+    assert np.abs(img - ref).max() <= TOL
