@@ -8,15 +8,26 @@ Workload (BASELINE.json configs[1]): Scene::Random (src/application.rs:497-565, 
   python bench.py                      # N=1, 3 timed frames after 1 warm-up
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 
-Multi-GPU: one process per GPU, no RCCL (control-plane barrier/max over gloo only).
-  --scaling weak   (default) every rank renders its own full 1920x1080x500 frame: the same image
-                   with the next 500 samples per pixel (sample_offset = rank*500) -- per-GPU work fixed.
-  --scaling strong the reference's 80x80 tiles of ONE frame dealt round-robin to the ranks
-                   (hrt_tile_grid), each rank rendering its tile set in one launch.
-Prints ONE JSON line on rank 0 (contract in the task statement).
+Multi-GPU (north star: the image tiled across the GPUs of one node, host gather, no RCCL): one process
+per GPU; gloo carries only the control plane (barrier, max of the timings) and the host gather.
+  --scaling tiles  (default) the frame's tile grid dealt to the ranks (hrt/tiling.py: 16-px tiles,
+                   diagonal interleave); each rank renders its share in one launch per step; after the
+                   timed steps the shares are gathered to rank 0 and the frame is checked bit for bit
+                   against a 1-GPU render of the whole frame.  Total work fixed: "scaling": "strong".
+  --scaling weak   replicas: every rank renders the whole frame with its own next spp samples per pixel.
+Rank 0 prints ONE JSON line (contract in the task statement), with
+  parity       per-pixel L-inf of the timed frame against the CPU oracle on a band of rows spread over
+               the frame, at the frame's full spp, plus equality of the ray counts (the metric's own
+               "per-pixel Linf vs CPU ref");
+  roofline     the kernel's real bound, VALU instruction issue (PMC counts of this build from
+               profiles/roofline_pmc.json over the live launch time), with the LDS / HBM figures beside it;
+  cpu_baseline the CPU restatement of the reference path (oracle/) on the same rows, timed on this
+               host's usable cores.
 """
 import argparse
+import hashlib
 import json
+import math
 import os
 import sys
 import time
@@ -27,9 +38,14 @@ sys.path.insert(0, os.path.join(ROOT, "hyper-ray-tracer_amd"))
 import torch  # noqa: E402  (first: libhrt binds to torch's HIP runtime)
 
 import hrt  # noqa: E402
+from hrt import tiling  # noqa: E402
 
-PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0     # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+PEAK_LDS_GBS = 150000.0   # ds_read_b64/b128 aggregate with every CU streaming (MI355X_MICROARCH.md, LDS)
+SIMDS, MAX_CLOCK_HZ = 1024, 2.4e9
+VALU_CYC = 2.0            # a wave64 VALU instruction issues over 2 cycles on a SIMD32 (MI355X_MICROARCH.md)
 EARTHMAP = os.path.join(ROOT, "tests", "golden", "earthmap_rgb8.png")  # the reference's assets/earthmap.jpg, decoded
+TOL = 1e-3                # north star: per-pixel L-inf <= 1e-3 vs the CPU reference
 
 
 def earth_image():
@@ -37,7 +53,7 @@ def earth_image():
     return hrt.load_image(EARTHMAP) if os.path.exists(EARTHMAP) else hrt.synthetic_earth()
 
 
-# algorithmic bytes of one traversal/shading step of THIS kernel (layout.h):
+# SURVEY 8(d) algorithmic bytes of one traversal / shading step (the reference model, this kernel's counts)
 NODE_B, PRIM_B, MAT_B, TEX_B, PIXEL_B = 32, 48, 32, 32, 16
 
 
@@ -51,11 +67,13 @@ def parse():
     ap.add_argument("--spp", type=int, default=500)
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--preset", default="random")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    ap.add_argument("--scaling", choices=["tiles", "weak"], default="tiles")
+    ap.add_argument("--tile", type=int, default=tiling.TILE, help="tile pitch of the multi-GPU split")
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline sample")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU-baseline / parity sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the CPU leg (and with it the parity band)")
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle parity band (profiling runs)")
+    ap.add_argument("--no-frame-check", action="store_true", help="N>1: skip the 1-GPU bit-identity check")
     ap.add_argument("--save", default="", help="write rank 0's last timed frame here (.pfm exact / .ppm 8-bit)")
     return ap.parse_args()
 
@@ -69,6 +87,20 @@ def host_cpu():
     except OSError:
         pass
     return "unknown"
+
+
+def usable_cpus():
+    """CPUs this process may actually use: its affinity set, capped by the cgroup CPU quota (the GPU
+    box exposes 256 host threads but grants one job a 16-CPU quota)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    return max(1, min(n, int(math.floor(quota)) if quota else n)), quota
 
 
 SCENE_LABEL = {  # BASELINE.json configs
@@ -91,45 +123,105 @@ def log(msg):
         print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def cpu_baseline(args, rank_segments_per_sample):
-    """The CPU restatement of the reference path (oracle/, 'port'), 80x80 tiles on a thread pool,
-    timed on this host on a bounded band of the same frame (rows through the middle of the image),
-    plus a one-thread rate on a short band."""
+def band_rows(H, n):
+    """n full-width rows spread evenly over the frame (the CPU sample and the parity band)."""
+    n = max(1, min(H, n))
+    return sorted({min(H - 1, int((k + 0.5) * H / n)) for k in range(n)})
+
+
+def cpu_leg(args, frame_rays_per_sample):
+    """The CPU restatement of the reference path (oracle/, 'port') on rows spread over the frame at the
+    frame's full spp, on this host's usable cores, plus a one-thread rate on a short
+    stretch.  Returns (cpu_baseline dict, rows, oracle image of the rows, oracle counters)."""
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
 
-    threads = min(16, os.cpu_count() or 1)
+    threads, quota = usable_cpus()
     o = O.OracleScene(hrt.PRESETS[args.preset], 1, earth_image())
     W, H = args.width, args.height
-    # calibrate on one row at a few spp, then size a band to ~cpu_seconds
+    # calibrate on a few rows at a few spp, then size the band to ~cpu_seconds
+    probe = band_rows(H, 4)
     t0 = time.perf_counter()
-    _, c = o.render(W, H, 8, args.depth, seed=args.seed, region=(0, H // 2, W, 1), threads=threads)
+    _, c = o.render_rows(W, H, 4, probe, args.depth, seed=args.seed, threads=threads)
     rate = c["segments"] / max(1e-6, time.perf_counter() - t0)
-    seg_per_row = c["segments"] / 8 * args.spp
-    rows = max(1, min(H // 2, int(args.cpu_seconds * rate / max(1.0, seg_per_row))))
-    y0 = H // 2 - rows // 2
+    rays_per_row = c["segments"] / (4 * len(probe)) * args.spp
+    n_rows = max(2, min(H, int(args.cpu_seconds * rate / max(1.0, rays_per_row))))
+    rows = band_rows(H, n_rows)
     t0 = time.perf_counter()
-    _, c = o.render(W, H, args.spp, args.depth, seed=args.seed, region=(0, y0, W, rows), threads=threads)
+    img, c = o.render_rows(W, H, args.spp, rows, args.depth, seed=args.seed, threads=threads)
     dt = time.perf_counter() - t0
-    # one thread, a short stretch of the middle row (~2 s)
-    px1 = max(8, min(W, int(2.0 * rate / threads / max(1.0, seg_per_row / W))))
+    # one thread, a stretch of the middle row (~2 s)
+    px1 = max(8, min(W, int(2.0 * rate / threads / max(1.0, rays_per_row / W))))
     t1 = time.perf_counter()
     _, c1 = o.render(W, H, args.spp, args.depth, seed=args.seed, region=(0, H // 2, px1, 1), threads=1)
     dt1 = time.perf_counter() - t1
-    return {
+    seg_per_sample = c["segments"] / max(1, c["samples"])
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    cb = {
         "value": round(c["segments"] / dt / 1e6, 4),
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
         "label": "CPU restatement of the reference path (oracle/, not the reference binary)",
-        "sample": f"rows {y0}..{y0 + rows - 1} of the {W}x{H} frame at {args.spp} spp "
+        "sample": f"{len(rows)} full-width rows spread evenly over the {W}x{H} frame at {args.spp} spp "
                   f"({c['samples']} samples, {c['segments']} rays, {dt:.1f} s); reference aabb.rs culling",
-        "segments_per_sample": round(c["segments"] / c["samples"], 4),
+        "segments_per_sample": round(seg_per_sample, 4),
+        "frame_segments_per_sample": round(frame_rays_per_sample, 4),
+        "sample_vs_frame": round(seg_per_sample / max(1e-9, frame_rays_per_sample), 4),
         "one_core_value": round(c1["segments"] / dt1 / 1e6, 4),
         "one_core_sample": f"{px1} pixels of row {H // 2} at {args.spp} spp ({c1['segments']} rays, {dt1:.1f} s)",
         "host_cpu": host_cpu(),
         "nproc": os.cpu_count(),
+        "cpu_quota": quota,
+        "threads_note": f"{threads} worker threads = the CPUs this job may use (affinity {aff}, "
+                        f"cgroup cpu.max quota {quota if quota else 'none'})",
     }
+    return cb, rows, img, c
+
+
+def roofline_obj(args, scene, cam, bg, tiles, p, out_ptr, stream, launch_ms, seg_step, n_px):
+    """The kernel's bound and where it sits (rank 0, instrumented pass outside the timed region)."""
+    pc = hrt.params(args.width, args.height, args.spp, args.depth, args.seed, bg, sample_offset=p.sample_offset,
+                    flags=hrt.RENDER_COUNT_WORK)
+    sc = hrt.render_tiles_device(scene, cam, pc, tiles, out_ptr, stream, want_stats=True)
+    launch_s = launch_ms * 1e-3
+    alg_bytes = (int(sc.node_visits) * NODE_B + int(sc.prim_tests) * PRIM_B + int(sc.segments) * MAT_B
+                 + int(sc.tex_evals) * TEX_B + n_px * PIXEL_B)
+    ro = {
+        "bound": "valu_issue",
+        "achieved": None, "peak": round(SIMDS * MAX_CLOCK_HZ / VALU_CYC / 1e9, 1), "unit": "Gwave-inst/s",
+        "frac": None, "traffic": None,
+        "walk_lane_util": round(int(sc.node_visits) / max(1, int(sc.walk_slots)), 4) if sc.walk_slots else None,
+        "alg_bytes_per_launch": alg_bytes,
+        "alg_bytes_per_ray": round(alg_bytes / max(1, seg_step), 1),
+        "lds_frac": round(alg_bytes / launch_s / 1e9 / PEAK_LDS_GBS, 4),
+        "node_visits_per_ray": round(int(sc.node_visits) / max(1, seg_step), 2),
+        "prim_tests_per_ray": round(int(sc.prim_tests) / max(1, seg_step), 3),
+        "launch_ms": round(launch_ms, 3),
+        "note": "achieved = SQ_INSTS_VALU of one launch of this build (rocprofv3 PMC, profiles/) / the live "
+                "HIP-event launch time; peak = 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction",
+    }
+    pj = os.path.join(ROOT, "profiles", "roofline_pmc.json")
+    key = f"{args.preset}_{args.width}x{args.height}_{args.spp}"
+    try:
+        pm = json.load(open(pj)).get(key)
+    except (OSError, ValueError):
+        pm = None
+    if pm and pm.get("valu_insts"):
+        sha = hashlib.sha256(open(hrt.LIB_PATH, "rb").read()).hexdigest()[:16]
+        ach = pm["valu_insts"] / launch_s / 1e9
+        ro.update(achieved=round(ach, 1), frac=round(ach / ro["peak"], 4), traffic=pm.get("hbm_bytes"),
+                  pmc_source=pm["source"], pmc_build_match=(pm.get("lib_sha16") == sha), lib_sha16=sha,
+                  valu_insts_per_launch=pm["valu_insts"], valu_insts_per_ray=round(pm["valu_insts"] / max(1, seg_step), 2))
+        if pm.get("clock_hz"):
+            ro["clock_ghz_profiled"] = round(pm["clock_hz"] / 1e9, 3)
+            ro["frac_at_profiled_clock"] = round(pm["valu_insts"] * VALU_CYC / (SIMDS * pm["clock_hz"] * launch_s), 4)
+        if pm.get("hbm_bytes"):
+            ro["hbm_counter_GBs"] = round(pm["hbm_bytes"] / launch_s / 1e9, 2)
+            ro["hbm_frac"] = round(pm["hbm_bytes"] / launch_s / 1e9 / PEAK_HBM_GBS, 5)
+        if pm.get("sq_lds_idx_active"):
+            ro["lds_bank_conflict_share"] = round(pm["sq_lds_bank_conflict"] / pm["sq_lds_idx_active"], 4)
+    return ro
 
 
 def main():
@@ -140,7 +232,7 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("gloo")  # control plane only: barrier + max of the timings
+        dist.init_process_group("gloo")  # control plane + host gather only (no RCCL, no device collective)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -150,13 +242,17 @@ def main():
     W, H = args.width, args.height
     cam = hrt.preset_camera(scene.info, W, H)
     bg = tuple(scene.info.background)
-    if args.scaling == "weak" or world == 1:
+    tiled = args.scaling == "tiles"
+    if world == 1:
+        tiles = [(0, 0, W, H)]  # the union of the grid: one launch over the frame
+        p = hrt.params(W, H, args.spp, args.depth, args.seed, bg)
+    elif tiled:
+        tiles = tiling.split_tiles(W, H, world, rank, args.tile)
+        p = hrt.params(W, H, args.spp, args.depth, args.seed, bg)
+    else:
         tiles = [(0, 0, W, H)]
         p = hrt.params(W, H, args.spp, args.depth, args.seed, bg, sample_offset=rank * args.spp)
-    else:
-        tiles = hrt.tile_grid(W, H, 80, rank, world)
-        p = hrt.params(W, H, args.spp, args.depth, args.seed, bg)
-    n_px = sum(t[2] * t[3] for t in tiles)
+    n_px = tiling.share_pixels(tiles)
     out = torch.empty(n_px * 4, dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
 
@@ -188,7 +284,9 @@ def main():
     torch.cuda.synchronize(dev)
     barrier()
     dt = time.perf_counter() - t0
+    scene.synchronize()  # raises if the walk watchdog stopped any timed launch (incomplete frame)
     launch_ms = sum(a.elapsed_time(b) for a, b in ev) / max(1, args.steps)
+    rank_ms = [round(launch_ms, 2)]
     if world > 1:
         import torch.distributed as dist
 
@@ -196,55 +294,61 @@ def main():
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        per = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(per, torch.tensor([launch_ms], dtype=torch.float64))
+        rank_ms = [round(float(x), 2) for x in per]
         dt, seg_all, samples_all = float(tmax[0]), float(t[1]), float(t[2])
     else:
         seg_all, samples_all = float(seg_step), float(samples_step)
-
     value = seg_all * args.steps / dt / 1e6
 
-    # algorithmic bytes of one launch (instrumented pass, rank 0, outside the timed region)
+    # N > 1, tile split: gather the shares to rank 0 (host, gloo) and check the frame bit for bit
+    frame_check = None
+    frame = None
+    if world > 1 and tiled:
+        tg = time.perf_counter()
+        frame = tiling.gather_frame(out.cpu().numpy(), W, H, world, rank,
+                                    shares=lambda r: tiling.split_tiles(W, H, world, r, args.tile))
+        gather_s = time.perf_counter() - tg
+        if rank == 0:
+            frame_check = {"gathered_pixels": int((frame[..., 3] == 1.0).sum()), "frame_pixels": W * H,
+                           "gather_ms": round(gather_s * 1e3, 1), "tile": args.tile,
+                           "rank_launch_ms": rank_ms, "imbalance": round(max(rank_ms) / max(1e-9, min(rank_ms)), 4)}
+            if not args.no_frame_check:
+                ref = torch.empty(W * H * 4, dtype=torch.float32, device=dev)
+                p1 = hrt.params(W, H, args.spp, args.depth, args.seed, bg)
+                hrt.render_tiles_device(scene, cam, p1, [(0, 0, W, H)], ref.data_ptr(), stream.cuda_stream)
+                torch.cuda.synchronize(dev)
+                same = bool((ref.view(H, W, 4).cpu().numpy() == frame).all())
+                frame_check["bit_identical_to_1gpu_frame"] = same
+                if not same:
+                    raise SystemExit("gathered multi-GPU frame differs from the 1-GPU frame")
+        barrier()
+    elif world == 1:
+        frame = out.view(H, W, 4)
+
+    cpu, parity = None, None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu, rows, ref_rows, cnt = cpu_leg(args, seg_step / max(1, samples_step))
+        if not args.no_parity:
+            got = out.view(H, W, 4)[torch.tensor(rows, device=dev)].cpu().numpy()
+            band_out = torch.empty(len(rows) * W * 4, dtype=torch.float32, device=dev)
+            band = hrt.render_tiles_device(scene, cam, p, [(0, y, W, 1) for y in rows], band_out.data_ptr(),
+                                           stream.cuda_stream, want_stats=True)
+            band_same = bool((band_out.view(len(rows), W, 4).cpu().numpy() == got).all())
+            linf = float(abs(got - ref_rows).max())
+            rays_equal = int(band.segments) == cnt["segments"]
+            parity = {"linf": linf, "tol": TOL, "pass": bool(linf <= TOL and rays_equal), "rays_equal": rays_equal,
+                      "gpu_rays": int(band.segments), "cpu_rays": cnt["segments"], "rows": len(rows),
+                      "pixels": len(rows) * W, "spp": args.spp, "band_render_equals_frame_rows": band_same,
+                      "reference": "oracle/ CPU restatement of the reference path, same seed and samples"}
+
     roofline = None
     if rank == 0:
-        pc = hrt.params(W, H, args.spp, args.depth, args.seed, bg, sample_offset=p.sample_offset, flags=hrt.RENDER_COUNT_WORK)
-        sc = hrt.render_tiles_device(scene, cam, pc, tiles, out.data_ptr(), stream.cuda_stream, want_stats=True)
-        shades = int(sc.segments)  # upper bound: one material fetch per segment that hit (misses fetch none)
-        alg_bytes = (int(sc.node_visits) * NODE_B + int(sc.prim_tests) * PRIM_B + shades * MAT_B
-                     + int(sc.tex_evals) * TEX_B + n_px * PIXEL_B)
-        achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
-        roofline = {
-            "bound": "hbm",
-            "achieved": round(achieved, 2),
-            "peak": PEAK_HBM_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / PEAK_HBM_GBS, 5),
-            "traffic": None,
-            "bytes_per_launch": alg_bytes,
-            "bytes_per_ray": round(alg_bytes / max(1, seg_step), 1),
-            "node_visits_per_ray": round(int(sc.node_visits) / max(1, seg_step), 2),
-            "prim_tests_per_ray": round(int(sc.prim_tests) / max(1, seg_step), 3),
-            "launch_ms": round(launch_ms, 3),
-        }
-        prof = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(prof):
-            try:
-                with open(prof) as fh:
-                    pm = json.load(fh)
-                key = f"{args.preset}_{W}x{H}_{args.spp}"
-                if key in pm:
-                    roofline["traffic"] = pm[key]["hbm_bytes_per_launch"]
-                    roofline["traffic_source"] = pm[key]["source"]
-            except (OSError, ValueError, KeyError):
-                pass
+        roofline = roofline_obj(args, scene, cam, bg, tiles, p, out.data_ptr(), stream.cuda_stream, launch_ms, seg_step, n_px)
 
-    if rank == 0 and args.save:
-        if tiles == [(0, 0, W, H)]:
-            hrt.write_image(args.save, out.view(H, W, 4).cpu().numpy())
-        else:
-            print("--save: rank 0 holds a tile set, not the frame; nothing written", file=sys.stderr)
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, seg_step / max(1, samples_step))
+    if rank == 0 and args.save and frame is not None:
+        hrt.write_image(args.save, frame.cpu().numpy() if torch.is_tensor(frame) else frame)
 
     if rank == 0:
         line = {
@@ -256,7 +360,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 2),
             "higher_is_better": True,
-            "scaling": "weak" if world == 1 or args.scaling == "weak" else "strong",
+            "scaling": "strong" if world > 1 and tiled else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": SCENE_DATA.get(args.preset, "synthetic (seeded scene builder)"),
@@ -266,12 +370,16 @@ def main():
                 "rays_per_step": int(seg_all), "samples_per_step": int(samples_all),
                 "rays_per_sample": round(seg_all / max(1.0, samples_all), 4),
                 "msamples_per_s": round(samples_all * args.steps / dt / 1e6, 2),
-                "parallelism": f"{world} GPU(s), {args.scaling} split, no collectives",
+                "parallelism": (f"{world} GPU(s), frame tiled ({args.tile}-px tiles, diagonal interleave), host gather, no collectives"
+                                if world > 1 and tiled else f"{world} GPU(s), " + ("replicas" if world > 1 else "one launch per frame")),
                 "cull_mode": {0: "reference", 1: "slab (approximate)", 2: "exact (reference test + provably safe culling)"}[si.cull_mode],
             },
+            "parity": parity,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        if frame_check is not None:
+            line["frame_check"] = frame_check
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

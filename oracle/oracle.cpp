@@ -33,6 +33,38 @@ using namespace hrt;
 
 namespace oracle {
 
+/* ---- the platform-libm variant (tests/test_libm.py) --------------------------------------------
+ * The reference's f32::{sin, cos, tan, acos, atan2, ln, powf} are calls into the platform libm: glibc's
+ * sinf / cosf / tanf / acosf / atan2f / logf / powf on Linux (Rust std lowers them to the C symbols).
+ * The restatement (and the kernel) use hd_math's deterministic f64 evaluations instead, which host and
+ * gfx950 compute bit for bit alike.  oracle_set_libm(1) switches THIS oracle to glibc's f32 functions,
+ * so the GPU frame can be compared with an oracle on the reference platform's arithmetic.  Optional
+ * input recording (single-threaded renders) collects the arguments the scenes actually produce. */
+static int g_libm = 0;
+enum { OP_SIN, OP_COS, OP_ACOS, OP_ATAN2, OP_LN, OP_POW5, OP_TAN, OP_N };
+static float* g_rec[OP_N] = {};
+static uint32_t g_rec_cap = 0;
+static std::atomic<uint32_t> g_rec_n[OP_N];
+static inline void rec1(int op, float a, float b = 0.0f) {
+  if (!g_rec[op]) return;
+  const uint32_t i = g_rec_n[op].fetch_add(1);
+  if (i < g_rec_cap) { g_rec[op][2 * i] = a; g_rec[op][2 * i + 1] = b; }
+}
+static inline float m_sin(float x) { rec1(OP_SIN, x); return g_libm ? sinf(x) : sin_f(x); }
+static inline float m_cos(float x) { rec1(OP_COS, x); return g_libm ? cosf(x) : cos_f(x); }
+static inline float m_tan(float x) { rec1(OP_TAN, x); return g_libm ? tanf(x) : tan_f(x); }
+static inline float m_acos(float x) { rec1(OP_ACOS, x); return g_libm ? acosf(x) : acos_f(x); }
+static inline float m_atan2(float y, float x) { rec1(OP_ATAN2, y, x); return g_libm ? atan2f(y, x) : atan2_f(y, x); }
+static inline float m_ln(float x) { rec1(OP_LN, x); return g_libm ? logf(x) : ln_f(x); }
+static inline float m_pow5(float x) { rec1(OP_POW5, x); return g_libm ? powf(x, 5.0f) : pow5_f(x); }
+/* math.rs:58-62 with the switchable powf */
+static inline float m_reflectance(float cosine, float refraction_index) {
+  float r0 = (1.0f - refraction_index) / (1.0f + refraction_index);
+  r0 = r0 * r0;
+  return r0 + (1.0f - r0) * m_pow5(1.0f - cosine);
+}
+
+
 static const float INF_F = u2f(0x7f800000u);
 
 /* ---------------------------------------------------------------- counters (instrumentation) */
@@ -123,7 +155,7 @@ struct CheckerTexture : Texture {
   CheckerTexture(TexP o, TexP e) : odd(std::move(o)), even(std::move(e)) {}
   Vec3 value(float u, float v, Vec3 p, Ctx& ctx) const override {
     ctx.cnt->c[C_TEX_CHECKER]++;
-    float sines = sin_f(10.0f * p.x) * sin_f(10.0f * p.y) * sin_f(10.0f * p.z);
+    float sines = m_sin(10.0f * p.x) * m_sin(10.0f * p.y) * m_sin(10.0f * p.z);
     if (sines < 0.0f) return odd->value(u, v, p, ctx);
     return even->value(u, v, p, ctx);
   }
@@ -216,7 +248,7 @@ struct NoiseTexture : Texture {
   NoiseTexture(std::shared_ptr<PerlinNoise> n, float s) : noise(std::move(n)), scale(s) {}
   Vec3 value(float, float, Vec3 p, Ctx& ctx) const override {
     ctx.cnt->c[C_TEX_NOISE]++;
-    float s = 1.0f + sin_f((scale * p.z) + (10.0f * noise->turbulence(scale * p, 7)));
+    float s = 1.0f + m_sin((scale * p.z) + (10.0f * noise->turbulence(scale * p, 7)));
     return (v3(1.0f, 1.0f, 1.0f) * 0.5f) * s;
   }
 };
@@ -297,7 +329,7 @@ struct Dielectric : Material {
     bool cannot_refract = (refraction_ratio * sin_theta) > 1.0f;
     Vec3 direction;
     /* the xi draw happens only when refraction is possible (|| short-circuits) */
-    if (cannot_refract || reflectance(cos_theta, refraction_ratio) > ctx.rng.gen_f32())
+    if (cannot_refract || m_reflectance(cos_theta, refraction_ratio) > ctx.rng.gen_f32())
       direction = reflect(unit_direction, rec.normal);
     else
       direction = refract(unit_direction, rec.normal, refraction_ratio);
@@ -337,8 +369,8 @@ using HitP = std::unique_ptr<Hittable>;
 
 /* sphere.rs:31-35 */
 static void sphere_uv(Vec3 p, float& u, float& v) {
-  float theta = acos_f(-p.y);
-  float phi = atan2_f(-p.z, p.x) + PI_F;
+  float theta = m_acos(-p.y);
+  float phi = m_atan2(-p.z, p.x) + PI_F;
   u = phi / (2.0f * PI_F);
   v = theta / PI_F;
 }
@@ -558,8 +590,8 @@ struct Rotation : Hittable {
     int r_axis, a_axis, b_axis;
     axes(axis, r_axis, a_axis, b_axis);
     float radians = (PI_F / 180.0f) * angle;
-    sin_theta = sin_f(radians);
-    cos_theta = cos_f(radians);
+    sin_theta = m_sin(radians);
+    cos_theta = m_cos(radians);
     Aabb b;
     has_box = hittable->bounding_box(0.0f, 1.0f, b);
     if (has_box) {
@@ -632,7 +664,7 @@ struct ConstantMedium : Hittable {
     float distance_inside_boundary = (r2.t - r1.t) * ray_length;
     /* rand.gen::<f32>().log(E) == ln(xi) / ln(E) (Rust f32::log) */
     float xi = medium_xi(ctx.pkey, ctx.segment, medium_id);
-    float hit_distance = negative_inverse_density * (ln_f(xi) / ln_f(E_F));
+    float hit_distance = negative_inverse_density * (m_ln(xi) / (g_libm ? logf(E_F) : ln_f(E_F)));
     if (hit_distance > distance_inside_boundary) return false;
     float t = r1.t + hit_distance / ray_length;
     rec.point = ray.at(t);
@@ -736,7 +768,7 @@ struct Camera {
   void resize(int width, int height) {
     float aspect_ratio = (float)width / (float)height;
     float theta = fov * (PI_F / 180.0f);
-    float h = tan_f(theta / 2.0f);
+    float h = m_tan(theta / 2.0f);
     float viewport_height = 2.0f * h;
     float viewport_width = aspect_ratio * viewport_height;
     w = normalize(look_from - look_at);
@@ -1194,6 +1226,58 @@ int oracle_render(void* scene, uint32_t W, uint32_t H, uint32_t spp, uint32_t de
   }
 }
 
+/* Columns [x0, x0 + w) of a set of rows of the W x H frame (bench.py's CPU baseline and parity band:
+ * full-width rows spread over the image, so the sample's rays per sample match the frame's; the GPU
+ * config tests: short windows of a row).  Same per-pixel computation as render(); the tasks are
+ * task_w-pixel row segments (80 = the reference's tile width) on the pool.  out: [n_rows][w][4]. */
+int oracle_render_rows(void* scene, uint32_t W, uint32_t H, uint32_t spp, uint32_t depth,
+                       uint32_t sample_offset, uint64_t seed, float t_min, const uint32_t* rows,
+                       uint32_t n_rows, uint32_t x0, uint32_t w, uint32_t task_w, float* out, int nthreads,
+                       uint64_t* counters) {
+  try {
+    Scene* s = static_cast<Scene*>(scene);
+    if (!s || !out || !rows || W < 2 || H < 2 || spp == 0 || w == 0 || task_w == 0 || x0 + w > W)
+      throw std::runtime_error("bad render arguments");
+    for (uint32_t r = 0; r < n_rows; r++)
+      if (rows[r] >= H) throw std::runtime_error("row outside the image");
+    const PresetInfo& I = s->info;
+    Camera cam(I.look_from, I.look_at, I.fov, I.aperture, I.focus_dist, I.time0, I.time1, (int)W, (int)H);
+    const uint32_t seg = task_w, per_row = (w + seg - 1) / seg, ntasks = per_row * n_rows;
+    std::atomic<uint32_t> next(0);
+    const int nt = nthreads > 0 ? nthreads : 1;
+    std::vector<Counters> per(nt);
+    std::vector<std::string> errs(nt);
+    auto worker = [&](int wid) {
+      try {
+        for (;;) {
+          const uint32_t t = next.fetch_add(1);
+          if (t >= ntasks) break;
+          const uint32_t r = t / per_row, lx = (t % per_row) * seg;
+          RenderArgs A{W, H, spp, depth, sample_offset, seed, t_min, x0 + lx, rows[r], std::min(seg, w - lx), 1u,
+                       out + 4 * ((size_t)r * w + lx)};
+          render(*s, cam, A, 1, per[wid]);
+        }
+      } catch (const std::exception& e) {
+        errs[wid] = e.what();
+      }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; t++) th.emplace_back(worker, t);
+    worker(0);
+    for (auto& t : th) t.join();
+    for (auto& e : errs)
+      if (!e.empty()) throw std::runtime_error(e);
+    Counters total;
+    for (auto& p : per)
+      for (int k = 0; k < C_COUNT; k++) total.c[k] += p.c[k];
+    if (counters) memcpy(counters, total.c, sizeof(total.c));
+    return 0;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return 1;
+  }
+}
+
 /* ---- unit entry points for the KAT fixtures (tests/golden) ---- */
 /* out: origin llc horizontal vertical u v w (21) lens_radius t0 t1 */
 void oracle_camera(const float* from, const float* at, float fov, float aperture, float focus,
@@ -1296,6 +1380,35 @@ void oracle_math(int op, const float* x, const float* y, float* out, uint32_t n)
     }
     out[i] = r;
   }
+}
+/* glibc's f32 functions (the reference platform's arithmetic), op as oracle_math */
+void oracle_math_libm(int op, const float* x, const float* y, float* out, uint32_t n) {
+  for (uint32_t i = 0; i < n; i++) {
+    float a = x[i], b = y ? y[i] : 0.0f, r = 0.0f;
+    switch (op) {
+      case 0: r = sinf(a); break;
+      case 1: r = cosf(a); break;
+      case 2: r = acosf(a); break;
+      case 3: r = atan2f(a, b); break;
+      case 4: r = logf(a); break;
+      case 5: r = powf(a, 5.0f); break;
+      case 6: r = tanf(a); break;
+    }
+    out[i] = r;
+  }
+}
+/* 1: renders (and scene builds) use glibc's f32 transcendentals; 0: hd_math (the kernel's) */
+void oracle_set_libm(int on) { g_libm = on ? 1 : 0; }
+/* Record the arguments of every transcendental call into bufs[op] (pairs (a, b), up to cap per op;
+ * bufs == NULL stops recording).  counts[op] receives the number of calls seen. */
+void oracle_record_math(float** bufs, uint32_t cap, uint32_t* counts) {
+  if (counts)
+    for (int k = 0; k < OP_N; k++) counts[k] = g_rec_n[k].load();
+  for (int k = 0; k < OP_N; k++) {
+    g_rec[k] = bufs ? bufs[k] : nullptr;
+    g_rec_n[k] = 0;
+  }
+  g_rec_cap = bufs ? cap : 0;
 }
 /* raw RNG streams: mode 0 gen_f32, 1 gen_range(-1,1), 2 next_u32 (as float bits) */
 void oracle_rng(uint64_t seed, uint32_t pixel, uint32_t sample, int mode, uint32_t n, float* out) {

@@ -42,6 +42,8 @@ def load() -> ctypes.CDLL:
     L.oracle_scene_bbox.argtypes = [vp, vp]
     L.oracle_render.restype = i32
     L.oracle_render.argtypes = [vp, u32, u32, u32, u32, u32, u64, f, u32, u32, u32, u32, vp, i32, vp]
+    L.oracle_render_rows.restype = i32
+    L.oracle_render_rows.argtypes = [vp, u32, u32, u32, u32, u32, u64, f, vp, u32, u32, u32, u32, vp, i32, vp]
     L.oracle_camera.argtypes = [vp, vp, f, f, f, f, f, i32, i32, vp]
     L.oracle_camera_ray.argtypes = [vp, vp, f, f, f, i32, i32, f, f, vp, f, vp]
     L.oracle_aabb_hit.restype = i32
@@ -54,6 +56,9 @@ def load() -> ctypes.CDLL:
     L.oracle_perlin_tables.argtypes = [u64, vp, vp]
     L.oracle_texture.argtypes = [i32, vp, f, f, f, vp, vp, vp, u32, u32, u32, vp]
     L.oracle_math.argtypes = [i32, vp, vp, vp, u32]
+    L.oracle_math_libm.argtypes = [i32, vp, vp, vp, u32]
+    L.oracle_set_libm.argtypes = [i32]
+    L.oracle_record_math.argtypes = [vp, u32, vp]
     L.oracle_rng.argtypes = [u64, u32, u32, i32, u32, vp]
     _lib = L
     return L
@@ -101,6 +106,20 @@ class OracleScene:
             raise RuntimeError(load().oracle_last_error().decode())
         return out, dict(zip(COUNTERS, [int(c) for c in cnt[: len(COUNTERS)]]))
 
+    def render_rows(self, width, height, spp, rows, depth=50, seed=1, threads=8, sample_offset=0, t_min=0.001,
+                    x0=0, w=None, task_w=80):
+        """Columns [x0, x0 + w) (default: all) of rows `rows` of the width x height frame, in tasks of
+        task_w pixels: (len(rows), w, 4) f32 and counters."""
+        r = np.ascontiguousarray(rows, np.uint32)
+        w = width - x0 if w is None else w
+        out = np.zeros((r.size, w, 4), np.float32)
+        cnt = np.zeros(16, np.uint64)
+        st = load().oracle_render_rows(self.h, width, height, spp, depth, sample_offset, seed, t_min, _p(r), r.size,
+                                       x0, w, task_w, _p(out), threads, _p(cnt))
+        if st != 0:
+            raise RuntimeError(load().oracle_last_error().decode())
+        return out, dict(zip(COUNTERS, [int(c) for c in cnt[: len(COUNTERS)]]))
+
 
 def math(op: int, x: np.ndarray, y: np.ndarray | None = None) -> np.ndarray:
     x = np.ascontiguousarray(x, np.float32)
@@ -108,3 +127,42 @@ def math(op: int, x: np.ndarray, y: np.ndarray | None = None) -> np.ndarray:
     yy = None if y is None else np.ascontiguousarray(y, np.float32)
     load().oracle_math(op, _p(x), None if yy is None else _p(yy), _p(out), x.size)
     return out
+
+
+def math_libm(op: int, x: np.ndarray, y: np.ndarray | None = None) -> np.ndarray:
+    """glibc's f32 function for op (0 sinf, 1 cosf, 2 acosf, 3 atan2f(x, y), 4 logf, 5 powf(x, 5), 6 tanf):
+    the reference platform's arithmetic (Rust f32 methods call these on Linux)."""
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.zeros_like(x)
+    yy = None if y is None else np.ascontiguousarray(y, np.float32)
+    load().oracle_math_libm(op, _p(x), None if yy is None else _p(yy), _p(out), x.size)
+    return out
+
+
+class libm_arithmetic:
+    """Context manager: oracle renders and scene builds inside use glibc's f32 transcendentals."""
+
+    def __enter__(self):
+        load().oracle_set_libm(1)
+        return self
+
+    def __exit__(self, *exc):
+        load().oracle_set_libm(0)
+        return False
+
+
+N_OPS = 7
+
+
+def record_math(fn, cap: int = 1 << 22):
+    """Run fn() (single-threaded oracle renders) and return {op: (n_calls, args[:min(n, cap), 2])}."""
+    bufs = [np.zeros(2 * cap, np.float32) for _ in range(N_OPS)]
+    ptrs = (ctypes.c_void_p * N_OPS)(*[b.ctypes.data for b in bufs])
+    counts = np.zeros(N_OPS, np.uint32)
+    L = load()
+    L.oracle_record_math(ptrs, cap, None)
+    try:
+        fn()
+    finally:
+        L.oracle_record_math(None, 0, counts.ctypes.data)
+    return {k: (int(counts[k]), bufs[k][: 2 * min(int(counts[k]), cap)].reshape(-1, 2)) for k in range(N_OPS)}

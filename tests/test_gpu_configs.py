@@ -1,0 +1,91 @@
+"""BASELINE.json's configs against the CPU oracle at their own sizes and sample counts (-m gpu).
+
+- C1 (configs[0]): Scene::Random 400x225, 50 spp, depth 50: the WHOLE frame, GPU vs oracle.
+- C2-C5 at full spp on bands of rows (the oracle runs ~1-40 Mrays/s on the box's 16 CPUs, so whole
+  1080p-4K frames at 500-10000 spp are out of its reach; bench.py checks C2's own frame on rows spread
+  over it): the GPU renders the same rows as tiles of the full-size image, with sample chunking, the
+  persistent kernel's work split and the LDS / global-memory scene paths of the real configuration.
+Bar: identical ray counts (world.hit calls) and per-pixel L-inf <= 1e-3 (north star)."""
+import numpy as np
+import pytest
+
+import hrt
+from oracle import oracle as O
+
+TOL = 1e-3
+THREADS = 16
+
+
+def _gpu_rows(name, W, H, spp, rows, earth, x0=0, w=None, seed=1):
+    import torch
+
+    s = hrt.preset(name, 1, earth)
+    s.commit()
+    cam = hrt.preset_camera(s.info, W, H)
+    w = W - x0 if w is None else w
+    p = hrt.params(W, H, spp, 50, seed, tuple(s.info.background))
+    d = torch.empty(len(rows) * w * 4, dtype=torch.float32, device="cuda")
+    st = hrt.render_tiles_device(s, cam, p, [(x0, y, w, 1) for y in rows], d.data_ptr(), 0, want_stats=True)
+    return d.view(len(rows), w, 4).cpu().numpy(), st
+
+
+@pytest.mark.gpu
+def test_c1_random_400x225_50spp_whole_frame(earth):
+    W, H, spp = 400, 225, 50
+    s = hrt.preset("random", 1, earth)
+    s.commit()
+    cam = hrt.preset_camera(s.info, W, H)
+    img, st = hrt.render(s, cam, hrt.params(W, H, spp, 50, 1, tuple(s.info.background)), stats=True)
+    ref, cnt = O.OracleScene(hrt.PRESETS["random"], 1, earth).render(W, H, spp, 50, seed=1, threads=THREADS)
+    assert st.pixels == W * H and st.samples == W * H * spp == cnt["samples"]
+    assert st.segments == cnt["segments"], (st.segments, cnt["segments"])
+    linf = float(np.abs(img - ref).max())
+    assert linf <= TOL, linf
+
+
+# (preset, W, H, spp, rows, x0, w): full-size image, full spp, rows spread over the frame
+BANDS = [
+    ("random", 1920, 1080, 500, [37, 540, 1001], 0, None),           # C2 (also bench.py's parity band)
+    ("earth_perlin", 1920, 1080, 1000, [100, 520, 700], 0, None),    # C3: image texture + Perlin ground
+    ("random_10k", 3840, 2160, 2000, [1080], 1856, 128),             # C4: 7 MB scene in global memory
+    ("cornell", 2048, 2048, 1250, [300, 1024, 1900], 0, None),       # C5: one GPU's share of 10000 spp
+    ("final", 800, 800, 200, [120, 400, 700], 0, None),              # Next-Week final (media, instances)
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,W,H,spp,rows,x0,w", BANDS)
+def test_config_band_full_spp(name, W, H, spp, rows, x0, w, earth):
+    img, st = _gpu_rows(name, W, H, spp, rows, earth, x0, w)
+    o = O.OracleScene(hrt.PRESETS[name], 1, earth)
+    ref, cnt = o.render_rows(W, H, spp, rows, 50, seed=1, threads=THREADS, x0=x0, w=w, task_w=8)
+    assert st.segments == cnt["segments"], (name, st.segments, cnt["segments"])
+    linf = float(np.abs(img - ref).max())
+    assert linf <= TOL, (name, linf)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_tiling_split_on_gpu(world, earth):
+    """bench.py's multi-GPU split on one GPU: every rank's share rendered in one launch (packed tiles),
+    placed by tiling.place_tiles, gives the 1-launch frame bit for bit."""
+    import torch
+
+    from hrt import tiling
+
+    W, H = 320, 180
+    s = hrt.preset("random", 1, earth)
+    s.commit()
+    cam = hrt.preset_camera(s.info, W, H)
+    p = hrt.params(W, H, 40, 50, 1, tuple(s.info.background))
+    full, st_full = hrt.render(s, cam, p, stats=True)
+    frame = np.full((H, W, 4), np.nan, np.float32)
+    segs = 0
+    for r in range(world):
+        t = tiling.split_tiles(W, H, world, r)
+        d = torch.empty(tiling.share_pixels(t) * 4, dtype=torch.float32, device="cuda")
+        st = hrt.render_tiles_device(s, cam, p, t, d.data_ptr(), 0, want_stats=True)
+        segs += int(st.segments)
+        tiling.place_tiles(frame, t, d.cpu().numpy())
+    assert segs == st_full.segments
+    assert np.array_equal(frame, full)

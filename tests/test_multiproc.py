@@ -1,17 +1,17 @@
-"""Multi-rank path on CPU (gloo, world_size 2): the tile split bench.py --scaling strong uses
-(hrt_tile_grid, round-robin over ranks) followed by a host-side gather reproduces the single-process
-frame bit for bit.  Each rank renders its tiles with the CPU oracle standing in for the GPU (the GPU
-equivalence of a tile set to the full frame is tests/test_gpu_parity.py::test_multi_tile_call...)."""
+"""Multi-rank path on CPU (gloo, world_size 2): bench.py's tile split (hrt/tiling.py split_tiles, the
+diagonal interleave of the 16-px grid) and its host gather (tiling.gather_frame, point-to-point over
+gloo) reassemble the single-process frame bit for bit.  Each rank renders its share with the CPU oracle
+standing in for its GPU (the GPU's packed tile output equals the full frame:
+tests/test_gpu_parity.py::test_multi_tile_call_matches_full_frame and ::test_tiling_split_on_gpu)."""
 import os
 import socket
 
 import numpy as np
 import pytest
-import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-W, H, SPP, DEPTH, SEED = 160, 90, 2, 8, 5
+W, H, SPP, DEPTH, SEED = 100, 45, 2, 8, 5
 
 
 def _free_port():
@@ -20,38 +20,42 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def _render_share(o, tiles):
+    """The packed layout hrt_render_tiles_device writes: tiles back to back, each row-major."""
+    parts, segs = [], 0
+    for t in tiles:
+        img, cnt = o.render(W, H, SPP, DEPTH, seed=SEED, region=t, threads=2)
+        parts.append(img.reshape(-1))
+        segs += cnt["segments"]
+    return np.concatenate(parts), segs
+
+
 def _worker(rank, world, port, q):
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [os.path.join(root, "hyper-ray-tracer_amd"), root]
+    import torch
+
     import hrt
+    from hrt import tiling
     from oracle import oracle as O
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     o = O.OracleScene(hrt.PRESETS["random"], 1)
-    tiles = hrt.tile_grid(W, H, 80, rank, world)
-    mine = []
-    for t in tiles:
-        img, cnt = o.render(W, H, SPP, DEPTH, seed=SEED, region=t, threads=2)
-        mine.append((t, img, cnt["segments"]))
-    gathered = [None] * world if rank == 0 else None
-    dist.gather_object(mine, gathered, dst=0)
+    packed, segs = _render_share(o, tiling.split_tiles(W, H, world, rank))
+    frame = tiling.gather_frame(packed, W, H, world, rank)
+    t = torch.tensor([float(segs)], dtype=torch.float64)
+    dist.all_reduce(t)
     if rank == 0:
-        frame = np.full((H, W, 4), np.nan, np.float32)
-        segs = 0
-        for part in gathered:
-            for (x, y, w, h), img, s in part:
-                frame[y:y + h, x:x + w] = img
-                segs += s
-        q.put((frame, segs))
+        q.put((frame, int(t.item())))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_two_rank_tile_split_matches_single_process(world):
+@pytest.mark.parametrize("world", [2, 3])
+def test_tile_split_and_gather_match_single_process(world):
     import hrt
     from oracle import oracle as O
 
@@ -65,3 +69,21 @@ def test_two_rank_tile_split_matches_single_process(world):
     assert not np.isnan(frame).any()
     assert np.array_equal(frame, ref)
     assert segs == cnt["segments"]
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_split_is_a_balanced_partition(world):
+    from hrt import tiling
+
+    Wf, Hf = 1920, 1080
+    allt = tiling.tile_grid(Wf, Hf)
+    parts = [tiling.split_tiles(Wf, Hf, world, r) for r in range(world)]
+    assert sorted(t for p in parts for t in p) == sorted(allt)
+    px = [tiling.share_pixels(p) for p in parts]
+    assert sum(px) == Wf * Hf
+    assert max(px) - min(px) <= 68 * 16 * 16  # at most one tile per tile row apart
+    # every rank's share covers the whole frame evenly: per horizontal band of 8 tile rows, shares agree
+    for r, p in enumerate(parts):
+        for band in range(0, Hf, 128):
+            n = sum(1 for t in p if band <= t[1] < band + 128)
+            assert abs(n - len([t for t in allt if band <= t[1] < band + 128]) / world) <= 8
