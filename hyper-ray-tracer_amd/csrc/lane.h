@@ -426,7 +426,7 @@ HRT_LANE void trace(const KParams& P, const G::Node* __restrict__ nodes, const G
     if (kind <= G::K_BOX_PRIM) {
       bool pass = box_hit<CULL>(a, b, r, tmin, closest, ref_only);
       if (kind == G::K_BOX) {
-        i = pass ? i + 1 : f2u(a.w);
+        i = pass ? i + 1 : umax(f2u(a.w), i + 1); /* skip links point forward: every walk ends */
         continue;
       }
       i++;

@@ -243,23 +243,27 @@ def test_progressive_tiles_assemble_the_frame(earth, batch, world):
 
 @pytest.mark.gpu
 def test_watchdog_reports_a_killed_frame_without_stats(earth):
-    """A corrupt skip link (a box node's fail link pointing back to the root) makes walks loop; the
+    """Corrupt skip links (box nodes' fail links pointing back to the root) make walks loop; the
     watchdog stops them, and the frame is reported HRT_ERR_STATE although the launch asked for no stats:
     by hrt_scene_synchronize, and by the call that next reuses the launch's scratch slot."""
-    import struct
-
     import torch
 
     s = hrt.preset("random", 1, earth)
     s.commit()
-    _, info = hrt.scene_blob(s)
     W, H = 64, 36
     cam = hrt.preset_camera(s.info, W, H)
     p = hrt.params(W, H, 2, 50, 3, tuple(s.info.background))
     ok, st = hrt.render(s, cam, p, stats=True)  # intact scene first
     assert st.pixels == W * H
-    # node 1 is the root's left child (a box node: pre-order); its skip link (dword 3) -> node 0
-    s.poke_blob(info.off_nodes + 32 * 1 + 12, struct.pack("<I", 0))
+    # every box node's fail link (dword 3) -> node 0: a ray that fails any box below the root walks
+    # back to the root and repeats the same walk for ever (a single corrupt link is not enough: the
+    # root's children contain the ground sphere's huge box, which nearly every ray passes)
+    buf, info = hrt.scene_blob(s)
+    nodes = np.frombuffer(buf.raw, np.uint32, count=8 * info.n_nodes, offset=info.off_nodes).reshape(-1, 8).copy()
+    boxed = ((nodes[:, 7] >> 24) & 0x7F) <= 1  # K_BOX, K_BOX_PRIM (layout.h)
+    assert boxed.sum() > 100
+    nodes[boxed, 3] = 0
+    s.poke_blob(info.off_nodes, nodes.tobytes())
     d = torch.zeros(W * H * 4, device="cuda")
     hrt.render_tiles_device(s, cam, p, [(0, 0, W, H)], d.data_ptr(), 0)  # no stats: returns at once
     with pytest.raises(hrt.HrtError) as e:
