@@ -71,6 +71,10 @@ struct KParams {
   uint32_t motion_uniform; /* every moving sphere has time0 = motion_t0, time1 - time0 = motion_span */
   float motion_t0, motion_span;
   float4* partial; /* [n_chunks][n_out] chunk sums (n_chunks > 1) */
+  /* sphere-scene walk stream (layout.h; render_basic_kernel under CULL_EXACT) */
+  const uint8_t* walk;
+  uint32_t walk_bytes; /* whole stream (what LDS staging copies) */
+  uint32_t walk_end;   /* byte offset one past the last record */
 };
 
 /* per-lane work counters of the instrumented (COUNT) instantiation */
@@ -292,20 +296,13 @@ HRT_LANE_FI bool box_infl(const float4& a, const float4& b, const TRay& r, float
 #endif
 }
 
-/* sphere.rs:38-55 / moving_sphere.rs:61-78: the accepted root only */
-HRT_LANE_FI bool sphere_root(const G::Prim* pp, uint32_t kind, const TRay& r, float tmin,
-                                            float tmax, float& root, bool motion_uniform) {
-  float4 p0 = ld4(pp->p0);
-  Vec3 c = v3(p0.x, p0.y, p0.z);
-  if (kind == G::P_MOVING) {
-    float4 p1 = ld4(pp->p1);
-    const float f = motion_uniform ? r.tau : (r.time - p1.w) / pp->p2[0];
-    c = c + f * v3(p1.x, p1.y, p1.z);
-  }
+/* sphere.rs:38-55 / moving_sphere.rs:61-78 for a sphere of centre c (at the ray's time) and radius
+ * `radius`: the accepted root only */
+HRT_LANE_FI bool sphere_root_at(Vec3 c, float radius, const TRay& r, float tmin, float tmax, float& root) {
   Vec3 oc = r.o - c;
   float a = r.dd;
   float half_b = dot(oc, r.d);
-  float cc = dot(oc, oc) - p0.w * p0.w;
+  float cc = dot(oc, oc) - radius * radius;
   float disc = half_b * half_b - a * cc;
   if (disc < 0.0f) return false;
   float sq = sqrtf(disc);
@@ -316,6 +313,19 @@ HRT_LANE_FI bool sphere_root(const G::Prim* pp, uint32_t kind, const TRay& r, fl
   }
   root = t;
   return true;
+}
+
+/* sphere.rs:38-55 / moving_sphere.rs:61-78: the accepted root only */
+HRT_LANE_FI bool sphere_root(const G::Prim* pp, uint32_t kind, const TRay& r, float tmin,
+                                            float tmax, float& root, bool motion_uniform) {
+  float4 p0 = ld4(pp->p0);
+  Vec3 c = v3(p0.x, p0.y, p0.z);
+  if (kind == G::P_MOVING) {
+    float4 p1 = ld4(pp->p1);
+    const float f = motion_uniform ? r.tau : (r.time - p1.w) / pp->p2[0];
+    c = c + f * v3(p1.x, p1.y, p1.z);
+  }
+  return sphere_root_at(c, p0.w, r, tmin, tmax, root);
 }
 
 HRT_LANE_FI void plane_axes(uint32_t plane, int& k, int& a, int& b) {
@@ -880,7 +890,7 @@ HRT_LANE_FI void init_path_state(PathState& ps) {
  * while the primitive of the leaf just passed (index - 1) waits for its test, or NONE when the lane
  * has no walk.  So "can step" is the single compare i < end, and the waiting primitive is read back
  * from the leaf's own record (basic_prim loads that record anyway for the reference test). */
-constexpr uint32_t WALK_PEND = 1u << 31;
+constexpr uint32_t WALK_PEND = G::WALK_PEND;
 HRT_LANE_FI bool walk_pending(uint32_t i) { return i - WALK_PEND < 0x7FFFFFFFu; } /* PEND set, i != NONE */
 
 /* A BASIC scene holds K_BOX, K_BOX_PRIM and K_PRIM nodes only (F_BASIC: no instances or media), so
@@ -956,6 +966,112 @@ HRT_LANE_FI void basic_step(const KParams& P, const G::Node* __restrict__ nodes,
                                            float& closest, uint32_t& winner, Counts& cn) {
   basic_box<CULL, COUNT>(P, nodes, i, r, closest, cn);
   if (walk_pending(i)) basic_prim<CULL, COUNT>(P, nodes, prims, i, r, closest, winner, cn);
+}
+
+/* ------------------------------------------------------------------ the sphere-scene walk stream */
+/* The walk of render_basic_kernel under CULL_EXACT, over the walk stream (layout.h): positions are
+ * byte offsets, read from LDS (the stream staged at LDS address 0), from global memory through a buffer
+ * descriptor (32-bit offsets, no 64-bit address arithmetic per step), or from a host pointer (the lane
+ * simulator). */
+enum : int { WM_LDS = 0, WM_BUF = 1, WM_HOST = 2 };
+struct WalkSrc {
+  const uint8_t* base; /* WM_BUF: the section in global memory; WM_HOST: the host copy */
+#if defined(__HIP_DEVICE_COMPILE__)
+  __amdgpu_buffer_rsrc_t rsrc; /* WM_BUF */
+#endif
+};
+
+template <int MEM>
+HRT_LANE_FI float4 wload(const WalkSrc& src, uint32_t off) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (MEM == WM_LDS) {
+    typedef __attribute__((address_space(3))) const float4 lds_float4;
+    return *(const lds_float4*)(size_t)off;
+  } else if constexpr (MEM == WM_BUF) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v v = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(src.rsrc, (int)off, 0, 0));
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
+#endif
+  return *reinterpret_cast<const float4*>(src.base + off);
+}
+
+/* The inflated test of CULL_EXACT on a box given by centre C and half-extent E (the walk stream's inner
+ * boxes, which hold the reference boxes): false only if the box, widened by EXACT_MARGIN x D' (D' =
+ * max_k |C_k - o_k| + E_k >= the L-inf distance of its farthest point from the origin), misses the ray
+ * on [tmin, tmax].  Per axis the slab is m_k -+ E_k |inv_k| with m_k = (C_k - o_k) inv_k, so the
+ * near/far swap of aabb.rs:28-29 disappears; the widening D' EXACT_MARGIN |inv_k| (= D' minv_k) is
+ * folded into one fma.  Rounding errors of the whole computation stay below ~6 2^-24 D' |inv_k|, far
+ * inside the slack of EXACT_MARGIN (layout.h: 4e-3 covers the 2.4e-3 needed 1.65 times).  A NaN bound
+ * (inv_k = +-inf: C_k = o_k or E_k = 0) is ignored by max3/min3: no constraint.  An infinite box
+ * (E = +inf) always passes. */
+HRT_LANE_FI bool box_ce(const float4& a, const float4& b, const TRay& r, float tmin, float tmax) {
+  const float C[3] = {a.x, a.y, a.z}, E[3] = {b.x, b.y, b.z};
+  const float o[3] = {r.o.x, r.o.y, r.o.z}, inv[3] = {r.inv.x, r.inv.y, r.inv.z};
+  const float mi[3] = {r.minv.x, r.minv.y, r.minv.z};
+  float m[3], e[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const float dc = C[k] - o[k];
+    m[k] = dc * inv[k];
+    e[k] = fabsf(dc) + E[k];
+  }
+  const float dist = fmaxf(fmaxf(e[0], e[1]), e[2]);
+  float l[3], h[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const float w = fmaf(dist, mi[k], E[k] * fabsf(inv[k]));
+    l[k] = m[k] - w;
+    h[k] = m[k] + w;
+  }
+  const float lo = fmaxf(fmaxf(l[0], l[1]), l[2]); /* NaN only if all three are: no constraint */
+  const float hi = fminf(fminf(h[0], h[1]), h[2]);
+  return !(hi < lo) & !(hi < tmin) & !(tmax < lo);
+}
+
+/* One node step: an inner node moves to pass / skip; a passed leaf parks the lane on it (WALK_PEND). */
+template <bool COUNT, int MEM>
+HRT_LANE_FI void walk_box(const WalkSrc& src, uint32_t& i, const TRay& r, float tmin, float closest, Counts& cn) {
+  const float4 a = wload<MEM>(src, i), b = wload<MEM>(src, i + 16u);
+  uint32_t skip = f2u(a.w);
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+v"(skip)); /* keep the link in the first 16-B load (see basic_box) */
+#endif
+  if constexpr (COUNT) cn.nodes++;
+  i = box_ce(a, b, r, tmin, closest) ? f2u(b.w) : skip;
+}
+
+/* The parked leaf's primitive: the reference test on its box (aabb.rs, monotone: leaves suffice, DESIGN
+ * section 4), then the sphere test against the lane's closest; the walk continues behind the leaf. */
+template <bool COUNT, int MEM>
+HRT_LANE_FI void walk_prim(const KParams& P, const WalkSrc& src, uint32_t& i, const TRay& r, float& closest,
+                           uint32_t& winner, Counts& cn) {
+  const uint32_t leaf = i - WALK_PEND;
+  i = leaf + G::WALK_LEAF_BYTES;
+  const float4 bmn = wload<MEM>(src, leaf + 32u), bmx = wload<MEM>(src, leaf + 48u);
+  const uint32_t w = f2u(bmn.w);
+  if (!(w & G::WL_NOBOX) && !box_ref(bmn, bmx, r, P.t_min, closest)) return;
+  if constexpr (COUNT) cn.prims++;
+  const float4 s0 = wload<MEM>(src, leaf + 64u);
+  Vec3 c = v3(s0.x, s0.y, s0.z);
+  if (w & G::WL_MOVING) { /* moving_sphere.rs:55-58 */
+    const float4 s1 = wload<MEM>(src, leaf + 80u);
+    const float f = P.motion_uniform ? r.tau : (r.time - s0.w) / s1.w;
+    c = c + f * v3(s1.x, s1.y, s1.z);
+  }
+  float t;
+  if (sphere_root_at(c, bmx.w, r, P.t_min, closest, t)) {
+    closest = t;
+    winner = w >> 2;
+  }
+}
+
+/* both halves back to back (the host lane simulator's walk) */
+template <bool COUNT>
+HRT_LANE_FI void walk_step_host(const KParams& P, const WalkSrc& src, uint32_t& i, const TRay& r, float& closest,
+                                uint32_t& winner, Counts& cn) {
+  walk_box<COUNT, WM_HOST>(src, i, r, P.t_min, closest, cn);
+  if (walk_pending(i)) walk_prim<COUNT, WM_HOST>(P, src, i, r, closest, winner, cn);
 }
 
 /* The BASIC kernel (sphere scenes: the Random family), with POSTPONED shading.  A lane's walk state

@@ -142,5 +142,27 @@ constexpr float EXACT_MARGIN = 4.0e-3f;
 constexpr uint32_t NODE_REF_ONLY = 1u << 31;
 constexpr uint32_t KIND_MASK = 0x7Fu;
 
+/* ---------------------------------------------------------------- sphere-scene walk stream
+ * What render_basic_kernel walks under CULL_EXACT: byte-addressed records in DFS pre-order, built at
+ * commit from the reference stream (scene.cpp build_walk).  Same leaves in the same order as the
+ * reference's BvhNode tree, so the walk tests the same primitives in the same order with the same
+ * closest; the inner boxes above them may be re-grouped (any hierarchy whose
+ * boxes contain their leaves' boxes gives the same result: the inflated test is conservative for any
+ * box that holds the geometry, and the reference test is applied at leaves).
+ *   inner (32 B): float4(C.xyz, skip)  float4(E.xyz, pass)
+ *   leaf  (96 B): float4(C.xyz, skip)  float4(E.xyz, pass)
+ *                 float4(mn.xyz, w)    float4(mx.xyz, radius)      the reference box (aabb.rs test)
+ *                 float4(c0.xyz, t0)   float4(c1 - c0, t1 - t0)    the sphere (moving_sphere.rs:55-58)
+ * C, E: centre and half-extent of a box holding the node's box ([C - E, C + E] contains [mn, mx] in
+ * real arithmetic: E rounded up), for the inflated test (lane.h box_ce).  skip = byte offset one past
+ * the subtree; pass = offset of the next node for an inner node, and (self | WALK_PEND) for a leaf: the
+ * lane parks on the leaf until the wave runs its primitive test (walk_prim), which continues at
+ * self + WALK_LEAF_BYTES.  w = WL_* flags | primitive index << 2 (the index of the prims section, the
+ * walk's winner).  A leaf without a reference box (a List member: K_PRIM) has C = 0, E = +inf (the
+ * inflated test always passes) and WL_NOBOX (no reference test). */
+constexpr uint32_t WALK_PEND = 1u << 31;
+constexpr uint32_t WALK_INNER_BYTES = 32, WALK_LEAF_BYTES = 96;
+constexpr uint32_t WL_MOVING = 1u, WL_NOBOX = 2u;
+
 }  // namespace gpu
 }  // namespace hrt

@@ -278,14 +278,36 @@ void render_basic_kernel(KParams P) {
   extern __shared__ float4 lds_scene[];
   const G::Node* nodes = P.nodes;
   const G::Prim* prims = P.prims;
-  /* with the scene in LDS the walk position is the node's LDS byte address (basic_box STRIDE) */
+  /* CULL_EXACT walks the walk stream (layout.h; positions are byte offsets, in LDS or through a buffer
+   * descriptor); the other modes walk the reference node stream (with the scene in LDS the walk
+   * position is the node's LDS byte address, basic_box STRIDE) */
+  constexpr bool WS = CULL == G::CULL_EXACT;
+  constexpr int WMEM = LDS ? WM_LDS : WM_BUF;
   constexpr uint32_t STRIDE = LDS ? (uint32_t)sizeof(G::Node) : 1u;
-  const uint32_t root = LDS ? (uint32_t)(size_t)(__attribute__((address_space(3))) float4*)lds_scene : 0u;
-  if constexpr (LDS) stage_scene<true>(P, lds_scene, nodes, prims, root);
+  const uint32_t lds_base = (uint32_t)(size_t)(__attribute__((address_space(3))) float4*)lds_scene;
+  const uint32_t root = WS || !LDS ? 0u : lds_base;
+  WalkSrc ws;
+  ws.base = P.walk;
+#if defined(__HIP_DEVICE_COMPILE__)
+  ws.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)P.walk, 0, (int)P.walk_bytes, 0x00020000);
+#endif
+  if constexpr (WS && LDS) { /* the stream at LDS address 0: its offsets are LDS addresses */
+    const float4* g = reinterpret_cast<const float4*>(P.walk);
+    for (uint32_t k = threadIdx.x; k < P.walk_bytes / 16u; k += blockDim.x) lds_scene[k] = g[k];
+    __syncthreads();
+    if (lds_base != 0u) { /* no static LDS in this kernel, so this cannot happen: report, do nothing */
+      if (threadIdx.x == 0) atomicOr(&P.stats[12], 2ull);
+      return;
+    }
+  } else if constexpr (LDS) {
+    stage_scene<true>(P, lds_scene, nodes, prims, root);
+  }
   const uint32_t lane = threadIdx.x & 63u;
   const float scale = 1.0f / (float)P.spp; /* application.rs:403 */
   const float inf = __uint_as_float(0x7f800000u);
-  const uint32_t end = root + P.main_end * STRIDE;
+  const uint32_t end = WS ? P.walk_end : root + P.main_end * STRIDE;
+  /* t_min canonicalised once: box_ce's fmaxf against it then needs no per-step quieting */
+  const float tmin_c = __builtin_canonicalizef(P.t_min);
   const uint32_t need = P.postpone;
   const uint32_t batch = P.prim_batch;
   /* watchdog: a lane's walk is at most walk_cap steps; waiting for a batch can stretch a pass to the
@@ -338,13 +360,19 @@ void render_basic_kernel(KParams P) {
 #pragma unroll
       for (int u = 0; u < WALK_UNROLL; u++) {
         if constexpr (COUNT) cn.walk_slots++;
-        if (node < end) basic_box<CULL, COUNT, STRIDE>(P, nodes, node, r, closest, cn);
+        if (node < end) {
+          if constexpr (WS) walk_box<COUNT, WMEM>(ws, node, r, tmin_c, closest, cn);
+          else basic_box<CULL, COUNT, STRIDE>(P, nodes, node, r, closest, cn);
+        }
         if ((u + 1) % PRIM_EVERY != 0) continue;
         const bool waiting = walk_pending(node);
         const unsigned long long pm = __ballot(waiting);
         if (pm && ((uint32_t)__popcll(pm) >= batch || !__ballot(node < end))) {
           if constexpr (COUNT) cn.prim_slots++;
-          if (waiting) basic_prim<CULL, COUNT, STRIDE>(P, nodes, prims, node, r, closest, winner, cn);
+          if (waiting) {
+            if constexpr (WS) walk_prim<COUNT, WMEM>(P, ws, node, r, closest, winner, cn);
+            else basic_prim<CULL, COUNT, STRIDE>(P, nodes, prims, node, r, closest, winner, cn);
+          }
         }
       }
       const unsigned long long live = __ballot(node < end || walk_pending(node));
@@ -606,7 +634,9 @@ void check_render_args(const hrt_camera* cam, const hrt_render_params* p) {
 void take_slot_error(hrt_scene::Slot& sl) {
   unsigned long long* h = (unsigned long long*)sl.h_tiles;
   if (h && h[12] != 0) {
+    const unsigned long long e = h[12];
     h[12] = 0;
+    if (e & 2ull) throw HipError{HRT_ERR_STATE, "the sphere kernel's LDS did not start at address 0 (walk stream not staged)"};
     throw HipError{HRT_ERR_STATE, SLOT_ERROR_MSG};
   }
 }
@@ -692,6 +722,8 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
             cam->time0 >= 0.0f && cam->time1 <= 1.0f;
   pl.smem = pl.fast ? (8 * (size_t)s->f_stream_len * sizeof(G::Node) + s->f_prims.size() * sizeof(G::Prim))
                     : (s->g_nodes.size() * sizeof(G::Node) + s->g_prims.size() * sizeof(G::Prim));
+  /* the sphere kernel under CULL_EXACT stages the walk stream (layout.h) instead */
+  if (!pl.full && !pl.fast && pl.cull == G::CULL_EXACT) pl.smem = s->w_end;
   pl.lds = (flags & HRT_RENDER_NO_LDS) == 0 && pl.smem <= (pl.fast ? LDS_FAST_MAX : LDS_SCENE_MAX);
   const char* k = getenv("HRT_KERNEL");
   /* General scenes run the segment-at-a-time kernel by default; render_full_kernel (persistent walks)
@@ -799,6 +831,9 @@ KParams scene_params(const hrt_scene* s, const hrt_camera* cam, const hrt_render
   kp.motion_uniform = s->motion_uniform ? 1u : 0u;
   kp.motion_t0 = s->motion_t0;
   kp.motion_span = s->motion_span;
+  kp.walk = base + s->off_walk;
+  kp.walk_bytes = s->w_end;
+  kp.walk_end = s->w_end;
   return kp;
 }
 

@@ -12,6 +12,8 @@
  *   counts           hittable/.rs count() (Rotation::count == 1, rotation.rs:140-142)
  */
 #include <algorithm>
+#include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -525,6 +527,185 @@ void build_fast(hrt_scene* s) {
   }
 }
 
+/* ------------------------------------------------------------------ sphere-scene walk stream */
+/* layout.h "sphere-scene walk stream": the records render_basic_kernel walks under CULL_EXACT.
+ *
+ * The leaves are the reference stream's leaves (K_BOX_PRIM: a BvhNode leaf, K_PRIM: a List member) in
+ * the reference's pre-order, so the walk tests the same primitives in the same order as BvhNode::hit
+ * (bvh_node.rs:104-127).  Above them, by default (HRT_WALK_TREE unset or "sah"), the inner boxes are
+ * RE-GROUPED: a top-down surface-area split of the fixed leaf sequence (each range cut where
+ * SA(left) n_left + SA(right) n_right is least).  The reference's own hierarchy splits on the longest
+ * axis of its node's box, which the r = 1000 ground sphere makes the y axis at every level that holds
+ * it, so its upper levels group spheres by height and every ray passes a chain of ground-sized boxes;
+ * the re-grouped tree puts the ground sphere alone under the root (64.4 -> ~53 node visits per ray on
+ * Random in a host simulation).  Any hierarchy over the same leaf sequence whose boxes hold their
+ * leaves' boxes gives the reference's result.  The reference hierarchy itself is
+ * kept (HRT_WALK_TREE=reference) for A/B, and whenever a leaf has no box or a box that is not a finite
+ * well-formed interval. */
+struct WalkLeaf {
+  Aabb box;
+  bool nobox;
+  uint32_t prim;
+};
+
+/* centre / half-extent of a box, E rounded up so that [C - E, C + E] holds [mn, mx] exactly */
+void box_ce_of(const Vec3& mn, const Vec3& mx, float* C, float* E) {
+  for (int k = 0; k < 3; k++) {
+    const double lo = mn[k], hi = mx[k];
+    const float c = (float)((lo + hi) * 0.5);
+    double e = std::max((double)c - lo, hi - (double)c);
+    e += e * 0x1p-50; /* the double differences are exact unless the exponents are far apart */
+    float ef = (float)e;
+    if ((double)ef < e) ef = nextafterf(ef, 3.40282347e+38f);
+    C[k] = c;
+    E[k] = ef;
+  }
+}
+
+struct WalkBuilder {
+  hrt_scene* s;
+  std::vector<float>& out;
+  uint32_t words() const { return (uint32_t)out.size(); }
+  uint32_t bytes() const { return 4u * words(); }
+  static void put4(std::vector<float>& o, float a, float b, float c, float d) {
+    o.push_back(a); o.push_back(b); o.push_back(c); o.push_back(d);
+  }
+  void inner(const Aabb& box, uint32_t skip) {
+    float C[3], E[3];
+    box_ce_of(box.mn, box.mx, C, E);
+    const uint32_t self = bytes();
+    put4(out, C[0], C[1], C[2], u2f(skip));
+    put4(out, E[0], E[1], E[2], u2f(self + G::WALK_INNER_BYTES));
+  }
+  void leaf(const WalkLeaf& L) {
+    const uint32_t self = bytes();
+    float C[3] = {0.0f, 0.0f, 0.0f}, E[3];
+    const float inf = u2f(0x7f800000u);
+    E[0] = E[1] = E[2] = inf;
+    if (!L.nobox) box_ce_of(L.box.mn, L.box.mx, C, E);
+    const G::Prim& p = s->g_prims[L.prim];
+    need(L.prim < (1u << 29), HRT_ERR_UNSUPPORTED, "too many primitives for the walk stream");
+    const bool moving = (p.km & 3u) == G::P_MOVING;
+    const uint32_t w = (moving ? G::WL_MOVING : 0u) | (L.nobox ? G::WL_NOBOX : 0u) | (L.prim << 2);
+    put4(out, C[0], C[1], C[2], u2f(self + G::WALK_LEAF_BYTES));
+    put4(out, E[0], E[1], E[2], u2f(self | G::WALK_PEND));
+    put4(out, L.box.mn.x, L.box.mn.y, L.box.mn.z, u2f(w));
+    put4(out, L.box.mx.x, L.box.mx.y, L.box.mx.z, p.p0[3]);
+    put4(out, p.p0[0], p.p0[1], p.p0[2], moving ? p.p1[3] : 0.0f);
+    put4(out, moving ? p.p1[0] : 0.0f, moving ? p.p1[1] : 0.0f, moving ? p.p1[2] : 0.0f, moving ? p.p2[0] : 1.0f);
+  }
+};
+
+uint32_t walk_subtree_bytes(uint32_t n_leaves) {
+  return (n_leaves - 1) * G::WALK_INNER_BYTES + n_leaves * G::WALK_LEAF_BYTES;
+}
+
+double half_area(const Aabb& b) {
+  const double x = (double)b.mx.x - b.mn.x, y = (double)b.mx.y - b.mn.y, z = (double)b.mx.z - b.mn.z;
+  return x * y + y * z + z * x;
+}
+
+Aabb box_union(const Aabb& a, const Aabb& b) {
+  Aabb u;
+  u.mn = v3(fminf(a.mn.x, b.mn.x), fminf(a.mn.y, b.mn.y), fminf(a.mn.z, b.mn.z));
+  u.mx = v3(fmaxf(a.mx.x, b.mx.x), fmaxf(a.mx.y, b.mx.y), fmaxf(a.mx.z, b.mx.z));
+  return u;
+}
+
+/* re-grouped hierarchy over leaves[0, n): iterative, pre-order (a range's bytes are known from its
+ * leaf count, so every skip link is written with its node) */
+void walk_regroup(WalkBuilder& B, const std::vector<WalkLeaf>& leaves) {
+  struct Range { uint32_t lo, hi; };
+  std::vector<Range> todo{{0u, (uint32_t)leaves.size()}};
+  std::vector<Aabb> pre, suf;
+  while (!todo.empty()) {
+    const Range r = todo.back();
+    todo.pop_back();
+    const uint32_t n = r.hi - r.lo;
+    if (n == 1) {
+      B.leaf(leaves[r.lo]);
+      continue;
+    }
+    pre.resize(n);
+    suf.resize(n);
+    pre[0] = leaves[r.lo].box;
+    for (uint32_t k = 1; k < n; k++) pre[k] = box_union(pre[k - 1], leaves[r.lo + k].box);
+    suf[n - 1] = leaves[r.hi - 1].box;
+    for (uint32_t k = n - 1; k-- > 0;) suf[k] = box_union(suf[k + 1], leaves[r.lo + k].box);
+    /* cut after leaf k (left = [lo, lo+k], right = the rest); ties go to the cut nearest the middle */
+    uint32_t best = (n - 1) / 2;
+    double best_cost = half_area(pre[best]) * (best + 1) + half_area(suf[best + 1]) * (n - 1 - best);
+    for (uint32_t k = 0; k + 1 < n; k++) {
+      const double c = half_area(pre[k]) * (k + 1) + half_area(suf[k + 1]) * (n - 1 - k);
+      const uint32_t dk = k > (n - 1) / 2 ? k - (n - 1) / 2 : (n - 1) / 2 - k;
+      const uint32_t db = best > (n - 1) / 2 ? best - (n - 1) / 2 : (n - 1) / 2 - best;
+      if (c < best_cost || (c == best_cost && dk < db)) {
+        best_cost = c;
+        best = k;
+      }
+    }
+    B.inner(pre[n - 1], B.bytes() + walk_subtree_bytes(n));
+    todo.push_back({r.lo + best + 1, r.hi}); /* right after left */
+    todo.push_back({r.lo, r.lo + best + 1});
+  }
+}
+
+void build_walk(hrt_scene* s) {
+  s->w_stream.clear();
+  s->w_end = 0;
+  s->w_regrouped = false;
+  if ((s->feature_mask & ~G::F_BASIC) != 0) return; /* sphere scenes only */
+  const uint32_t n = s->main_end;
+  std::vector<WalkLeaf> leaves;
+  bool regroup_ok = true;
+  for (uint32_t i = 0; i < n; i++) {
+    const G::Node& g = s->g_nodes[i];
+    const uint32_t kind = (g.kp >> 24) & G::KIND_MASK;
+    if (kind == G::K_BOX) continue;
+    need(kind == G::K_BOX_PRIM || kind == G::K_PRIM, HRT_ERR_STATE, "walk stream: unexpected node kind");
+    WalkLeaf L;
+    L.nobox = kind == G::K_PRIM;
+    L.prim = g.kp & 0xFFFFFFu;
+    L.box.mn = v3(g.mn[0], g.mn[1], g.mn[2]);
+    L.box.mx = v3(g.mx[0], g.mx[1], g.mx[2]);
+    if (L.nobox) regroup_ok = false;
+    for (int k = 0; k < 3 && !L.nobox; k++)
+      if (!(g.mn[k] <= g.mx[k]) || !std::isfinite(g.mn[k]) || !std::isfinite(g.mx[k])) regroup_ok = false;
+    leaves.push_back(L);
+  }
+  if (leaves.empty()) return;
+  const char* mode = getenv("HRT_WALK_TREE");
+  const bool regroup = regroup_ok && !(mode && strcmp(mode, "reference") == 0);
+  WalkBuilder B{s, s->w_stream};
+  if (regroup) {
+    walk_regroup(B, leaves);
+    s->w_regrouped = true;
+  } else { /* the reference hierarchy, record for record */
+    std::vector<uint32_t> at(n + 1); /* node index -> byte offset */
+    uint32_t off = 0;
+    for (uint32_t i = 0; i < n; i++) {
+      at[i] = off;
+      off += ((s->g_nodes[i].kp >> 24) & G::KIND_MASK) == G::K_BOX ? G::WALK_INNER_BYTES : G::WALK_LEAF_BYTES;
+    }
+    at[n] = off;
+    size_t li = 0;
+    for (uint32_t i = 0; i < n; i++) {
+      const G::Node& g = s->g_nodes[i];
+      if (((g.kp >> 24) & G::KIND_MASK) == G::K_BOX) {
+        Aabb b;
+        b.mn = v3(g.mn[0], g.mn[1], g.mn[2]);
+        b.mx = v3(g.mx[0], g.mx[1], g.mx[2]);
+        need(g.skip > i && g.skip <= n, HRT_ERR_STATE, "walk stream: bad skip link");
+        B.inner(b, at[g.skip]);
+      } else {
+        B.leaf(leaves[li++]);
+      }
+    }
+  }
+  s->w_end = B.bytes();
+  need(s->w_end == walk_subtree_bytes((uint32_t)leaves.size()) || !regroup, HRT_ERR_STATE, "walk stream size");
+}
+
 void flatten(hrt_scene* s) {
   s->g_nodes.clear(); s->g_prims.clear(); s->g_insts.clear(); s->g_media.clear();
   s->g_mats.clear(); s->g_texs.clear();
@@ -597,6 +778,7 @@ void flatten(hrt_scene* s) {
   s->f_prims.clear();
   s->f_stream_len = 0;
   if (sphere_only && (s->feature_mask & ~G::F_BASIC) == 0) build_fast(s); /* opt-in approximate path */
+  build_walk(s);
 }
 
 }  // namespace
@@ -624,6 +806,7 @@ std::vector<uint8_t> build_blob(hrt_scene* s) {
   s->off_images = section(s->images.size());
   s->off_fnodes = section(s->f_nodes.size() * sizeof(G::Node));
   s->off_fprims = section(s->f_prims.size() * sizeof(G::Prim));
+  s->off_walk = section(s->w_stream.size() * sizeof(float));
   s->blob_bytes = off;
   std::vector<uint8_t> blob(off, 0);
   auto put = [&](size_t o, const void* src, size_t bytes) {
@@ -639,6 +822,7 @@ std::vector<uint8_t> build_blob(hrt_scene* s) {
   put(s->off_images, s->images.data(), s->images.size());
   put(s->off_fnodes, s->f_nodes.data(), s->f_nodes.size() * sizeof(G::Node));
   put(s->off_fprims, s->f_prims.data(), s->f_prims.size() * sizeof(G::Prim));
+  put(s->off_walk, s->w_stream.data(), s->w_stream.size() * sizeof(float));
   return blob;
 }
 }  // namespace hrt
@@ -1044,6 +1228,9 @@ hrt_status hrt_debug_scene_blob(hrt_scene* s, void* out, uint64_t cap, uint64_t*
       info->media_nested = s->media_nested ? 1u : 0u;
       info->box_t0 = s->box_t0;
       info->box_t1 = s->box_t1;
+      info->off_walk = s->off_walk;
+      info->walk_bytes = s->w_end;
+      info->walk_regrouped = s->w_regrouped ? 1u : 0u;
     }
   });
 }

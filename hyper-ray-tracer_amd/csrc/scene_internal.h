@@ -90,6 +90,11 @@ struct hrt_scene {
   std::vector<hrt::gpu::Prim> f_prims;
   uint32_t f_stream_len = 0;
   size_t off_fnodes = 0, off_fprims = 0;
+  /* sphere-scene walk stream (layout.h; render_basic_kernel under CULL_EXACT): byte records */
+  std::vector<float> w_stream;
+  uint32_t w_end = 0;        /* bytes */
+  bool w_regrouped = false;  /* inner boxes re-grouped over the reference leaf order (build_walk) */
+  size_t off_walk = 0;
   uint32_t feature_mask = 0;
   int cull_mode = hrt::gpu::CULL_REFERENCE;
   bool all_boxes_ok = true;         /* no NODE_REF_ONLY node (slab culling is geometrically safe) */

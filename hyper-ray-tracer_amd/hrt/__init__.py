@@ -102,7 +102,8 @@ class BlobInfo(ctypes.Structure):
                                                 "off_perlin", "off_images")] + \
         [(n, ctypes.c_uint32) for n in ("n_nodes", "main_end", "n_prims", "feature_mask", "cull_mode", "motion_uniform")] + \
         [("motion_t0", ctypes.c_float), ("motion_span", ctypes.c_float), ("ln_e", ctypes.c_float),
-         ("media_nested", ctypes.c_uint32), ("box_t0", ctypes.c_float), ("box_t1", ctypes.c_float)]
+         ("media_nested", ctypes.c_uint32), ("box_t0", ctypes.c_float), ("box_t1", ctypes.c_float),
+         ("off_walk", ctypes.c_uint64), ("walk_bytes", ctypes.c_uint32), ("walk_regrouped", ctypes.c_uint32)]
 
 
 class PresetInfo(ctypes.Structure):

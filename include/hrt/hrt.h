@@ -291,6 +291,9 @@ typedef struct hrt_blob_info {
   float ln_e;
   uint32_t media_nested;   /* a ConstantMedium inside a Translation/Rotation */
   float box_t0, box_t1;    /* ray times the BVH boxes are valid for */
+  uint64_t off_walk;       /* sphere scenes: the walk stream of the default (exact) sphere kernel */
+  uint32_t walk_bytes;     /* its size (0: not a sphere scene) */
+  uint32_t walk_regrouped; /* its inner boxes re-grouped over the reference leaf order */
 } hrt_blob_info;
 hrt_status hrt_debug_scene_blob(hrt_scene* s, void* out, uint64_t cap, uint64_t* size, hrt_blob_info* info);
 /* Overwrite n bytes of the committed scene's DEVICE blob at byte `offset` (hrt_blob_info offsets), after

@@ -3,7 +3,8 @@
  * on the host, one lane at a time, over the flattened scene of hrt_debug_scene_blob.
  *
  * A GPU lane of render_basic_kernel / render_full_kernel executes, for each of its samples, exactly:
- * start_sample -> { walk to the end with basic_step / full_step; shade } until the path ends, and
+ * start_sample -> { walk to the end with walk_box/walk_prim (the sphere kernel under CULL_EXACT, over the
+ * walk stream), basic_step or full_step; shade } until the path ends, and
  * sums the samples of a chunk in order (reduce_chunks then adds the chunk sums in chunk order).
  * Which lanes step together, and when a wave stops to shade, never changes a lane's own sequence of
  * tests and draws.  So this harness reproduces what the kernels compute per pixel, and
@@ -65,7 +66,13 @@ void render_pixel(const KParams& P, uint32_t px, uint32_t py, float* rgba, uint6
         } else {
           uint32_t node = ps.depth_left == 0 ? G::NONE : 0u, winner = G::NONE;
           float closest = inf;
-          while (node < P.main_end) basic_step<CULL, true>(P, P.nodes, P.prims, node, r, closest, winner, cn);
+          if constexpr (CULL == G::CULL_EXACT) { /* the walk stream (layout.h), as the kernel walks it */
+            WalkSrc src;
+            src.base = P.walk;
+            while (node < P.walk_end) walk_step_host<true>(P, src, node, r, closest, winner, cn);
+          } else {
+            while (node < P.main_end) basic_step<CULL, true>(P, P.nodes, P.prims, node, r, closest, winner, cn);
+          }
           traced = node != G::NONE;
           done = !traced ||
                  shade<false, true>(P, ps, winner, closest, r.o, r.d, r.time, r.tau, cn) || ps.depth_left == 0;
@@ -117,6 +124,9 @@ int lane_sim_render(const void* blob, const hrt_blob_info* bi, const hrt_camera*
   P.motion_uniform = bi->motion_uniform;
   P.motion_t0 = bi->motion_t0;
   P.motion_span = bi->motion_span;
+  P.walk = base + bi->off_walk;
+  P.walk_bytes = bi->walk_bytes;
+  P.walk_end = bi->walk_bytes;
   P.cam_origin = v3(cam->origin[0], cam->origin[1], cam->origin[2]);
   P.cam_llc = v3(cam->lower_left_corner[0], cam->lower_left_corner[1], cam->lower_left_corner[2]);
   P.cam_h = v3(cam->horizontal[0], cam->horizontal[1], cam->horizontal[2]);

@@ -264,6 +264,18 @@ def test_watchdog_reports_a_killed_frame_without_stats(earth):
     assert boxed.sum() > 100
     nodes[boxed, 3] = 0
     s.poke_blob(info.off_nodes, nodes.tobytes())
+    # the sphere kernel's walk stream (layout.h): every inner record's skip link -> offset 0 (the root)
+    assert info.walk_bytes > 0
+    ws = np.frombuffer(buf.raw, np.uint32, count=info.walk_bytes // 4, offset=info.off_walk).copy()
+    off, inner = 0, 0
+    while off < info.walk_bytes:
+        leaf = (ws[off // 4 + 7] & 0x80000000) != 0  # pass link with WALK_PEND: a leaf (96 B)
+        if not leaf:
+            ws[off // 4 + 3] = 0
+            inner += 1
+        off += 96 if leaf else 32
+    assert inner > 100
+    s.poke_blob(info.off_walk, ws.tobytes())
     d = torch.zeros(W * H * 4, device="cuda")
     hrt.render_tiles_device(s, cam, p, [(0, 0, W, H)], d.data_ptr(), 0)  # no stats: returns at once
     with pytest.raises(hrt.HrtError) as e:

@@ -155,3 +155,22 @@ def test_headline_frame_band_at_500_spp(sim, earth):
     assert st["samples"] == 1920 * 2 * 500
     assert st["segments"] == cnt["segments"]
     assert np.abs(img - ref).max() <= TOL
+
+
+@pytest.mark.parametrize("name", ["random", "random_10k", "two_spheres"])
+def test_walk_stream_regrouped_equals_reference_hierarchy(sim, earth, name, monkeypatch):
+    """The sphere kernel's walk stream re-groups the inner boxes over the reference's leaf order
+    (scene.cpp build_walk): bit-identical to the walk over the reference hierarchy, with fewer node visits."""
+    a, sa = sim_render(sim, name, 48, 27, 4, 50, 5, earth, kernel=0, cull=CULL_EXACT)
+    monkeypatch.setenv("HRT_WALK_TREE", "reference")
+    b, sb = sim_render(sim, name, 48, 27, 4, 50, 5, earth, kernel=0, cull=CULL_EXACT)
+    assert sa["segments"] == sb["segments"] and sa["prims"] == sb["prims"]
+    assert np.array_equal(a, b)
+    _, info = hrt.scene_blob(hrt.preset(name, 1, earth))
+    assert info.walk_regrouped == 0 and info.walk_bytes > 0
+    monkeypatch.delenv("HRT_WALK_TREE")
+    _, info = hrt.scene_blob(hrt.preset(name, 1, earth))
+    assert info.walk_regrouped == 1
+    if name != "two_spheres":  # (two leaves: nothing to re-group)
+        assert sa["nodes"] < 0.95 * sb["nodes"], (sa["nodes"], sb["nodes"])
+    print(name, "node visits: re-grouped", sa["nodes"], "reference hierarchy", sb["nodes"])
