@@ -149,6 +149,35 @@ HRT_LANE_FI void set_ray(TRay& r, Vec3 o, Vec3 d, float time, const KParams& P) 
 
 HRT_LANE_FI float4 ld4(const void* p) { return *reinterpret_cast<const float4*>(p); }
 
+/* ------------------------------------------------------------------ the sphere-scene walk stream */
+/* The walk of render_basic_kernel under CULL_EXACT, over the walk stream (layout.h): positions are
+ * byte offsets, read from LDS (the stream staged at LDS address 0), from global memory through a buffer
+ * descriptor (32-bit offsets, no 64-bit address arithmetic per step), or from a host pointer (the lane
+ * simulator). */
+enum : int { WM_LDS = 0, WM_BUF = 1, WM_HOST = 2 };
+struct WalkSrc {
+  const uint8_t* base; /* WM_BUF: the section in global memory; WM_HOST: the host copy */
+#if defined(__HIP_DEVICE_COMPILE__)
+  __amdgpu_buffer_rsrc_t rsrc; /* WM_BUF */
+#endif
+};
+
+template <int MEM>
+HRT_LANE_FI float4 wload(const WalkSrc& src, uint32_t off) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (MEM == WM_LDS) {
+    typedef __attribute__((address_space(3))) const float4 lds_float4;
+    return *(const lds_float4*)(size_t)off;
+  } else if constexpr (MEM == WM_BUF) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v v = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(src.rsrc, (int)off, 0, 0));
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
+#endif
+  return *reinterpret_cast<const float4*>(src.base + off);
+}
+
+
 /* aabb.rs:20-47 (CULL_REFERENCE), its narrowed form (CULL_SLAB), or CULL_EXACT: the reference test
  * AND an inflated slab test that only rejects boxes no accepted hit can come from (layout.h).
  * `if t0 > t_min {t0} else {t_min}` (aabb.rs:30-35) is fmaxf(t0, t_min): in IEEE mode v_max_f32
@@ -662,6 +691,9 @@ HRT_LANE_NI bool checker_product_negative(float vx, float vy, float vz) {
  * product of three cannot underflow, so the product is negative exactly when an odd number of
  * factors are; anything else (zero, tiny, huge, NaN) takes sin_f's full product. */
 HRT_LANE_FI bool checker_odd(float vx, float vy, float vz) {
+#if HRT_EXP_NOCHECKER /* timing experiment only (wrong colours): the price of the sine signs */
+  return vx < 0.0f;
+#endif
   const float ax = fabsf(vx), ay = fabsf(vy), az = fabsf(vz);
   const bool in_range = ax >= 1e-6f && ax <= 1e6f && ay >= 1e-6f && ay <= 1e6f && az >= 1e-6f && az <= 1e6f;
   if (in_range) return sin_negative(vx) != (sin_negative(vy) != sin_negative(vz));
@@ -744,9 +776,17 @@ inline void set_pixel_rcp(KParams& P) {
 
 HRT_LANE_FI void start_sample(const KParams& P, PathState& ps, uint32_t px, uint32_t py,
                                              uint32_t sample) {
+#if HRT_EXP_CHEAPSEED /* timing experiment only (wrong streams): the price of the per-sample seeding */
+  {
+    const uint32_t k = (py * P.W + px) * 0x9E3779B9u ^ (P.sample_offset + sample) * 0x85EBCA6Bu;
+    ps.pk.pkey = k;
+    ps.rng.s0 = k | 1u; ps.rng.s1 = k ^ 0x6A09E667u; ps.rng.s2 = k ^ 0xBB67AE85u; ps.rng.s3 = k ^ 0x3C6EF372u;
+  }
+#else
   ps.pk.pkey = path_key(P.seed, py * P.W + px, P.sample_offset + sample);
-  ps.pk.segment = 0;
   ps.rng = rng_from_key(ps.pk.pkey);
+#endif
+  ps.pk.segment = 0;
   /* application.rs:444-445 u, v: x / (W - 1) correctly rounded by div_rn's 3-instruction core with the
    * host's y = RN(1 / a), a = W - 1, and no IEEE fallback.  Why that is exact here (render parameters
    * hold 2 <= W, H <= 65535, so a is an integer in [1, 65534]; x = RN(px + gen_f32()) is 0 or an f32
@@ -775,18 +815,13 @@ HRT_LANE_FI void start_sample(const KParams& P, PathState& ps, uint32_t px, uint
   ps.depth_left = P.max_depth;
 }
 
-/* The part of one ray_color step after world.hit (application.rs:483-494): background on a miss,
- * else hit record, emission and scatter.  (ro, rd, rtime) is the segment just traced; the scattered
- * ray goes to ps.ro/ps.rd.  Returns true when the path is finished. */
-template <bool FULL, bool COUNT>
-HRT_LANE_FI bool shade(const KParams& P, PathState& ps, uint32_t winner, float closest, Vec3 ro,
-                                      Vec3 rd, float rtime, float tau, Counts& cn) {
-  if (winner == G::NONE) {
-    ps.rad = ps.rad + mul_elem(ps.thr, P.background);
-    return true;
-  }
-  Rec rec = make_record<FULL>(P, winner, closest, ro, rd, rtime, tau);
-  const G::Mat M = P.mats[rec.mat];
+/* The scatter of one ray_color step (application.rs:486-494) at the hit `rec` of a material of kind
+ * `kind` (Metal: albedo, fuzz; Dielectric: ior); `tex()` is the material's texture at the hit (read
+ * after the scatter's draws: textures draw no random numbers).  The scattered ray goes to
+ * ps.ro/ps.rd.  Returns true when the path is finished. */
+template <bool FULL, class TexFn>
+HRT_LANE_FI bool scatter(PathState& ps, const Rec& rec, uint32_t kind, Vec3 albedo, float fuzz, float ior, Vec3 rd,
+                         TexFn&& tex) {
   Vec3 emitted = v3(0.0f, 0.0f, 0.0f);
   Vec3 att = v3(0.0f, 0.0f, 0.0f), ndir = v3(0.0f, 0.0f, 0.0f);
   bool scattered = false;
@@ -796,20 +831,20 @@ HRT_LANE_FI bool shade(const KParams& P, PathState& ps, uint32_t winner, float c
    * reflect draws nothing): ONE rejection loop shared by the three branches, so a wave holding several
    * of these materials runs the loop once, not once per branch. */
   Vec3 sph = v3(0.0f, 0.0f, 0.0f);
-  if (M.kind == G::M_LAMBERTIAN || M.kind == G::M_METAL || (FULL && M.kind == G::M_ISOTROPIC))
+  if (kind == G::M_LAMBERTIAN || kind == G::M_METAL || (FULL && kind == G::M_ISOTROPIC))
     sph = random_in_unit_sphere(rng);
-  if (M.kind == G::M_LAMBERTIAN) { /* lambertian.rs:27-38 */
+  if (kind == G::M_LAMBERTIAN) { /* lambertian.rs:27-38 */
     ndir = rec.n + normalize(sph); /* random_unit_vector, math.rs:12-14 */
     if (near_zero(ndir)) ndir = rec.n;
     textured = true;
     scattered = true;
-  } else if (M.kind == G::M_METAL) { /* metal.rs:29-42 */
+  } else if (kind == G::M_METAL) { /* metal.rs:29-42 */
     Vec3 reflected = reflect(normalize(rd), rec.n);
-    ndir = reflected + M.a[3] * sph;
+    ndir = reflected + fuzz * sph;
     scattered = dot(ndir, rec.n) > 0.0f;
-    att = v3(M.a[0], M.a[1], M.a[2]);
-  } else if (M.kind == G::M_DIELECTRIC) { /* dielectric.rs:31-55 */
-    float ratio = rec.front ? (1.0f / M.a[0]) : M.a[0];
+    att = albedo;
+  } else if (kind == G::M_DIELECTRIC) { /* dielectric.rs:31-55 */
+    float ratio = rec.front ? (1.0f / ior) : ior;
     Vec3 ud = normalize(rd);
     float cos_theta = min_rs(dot(-ud, rec.n), 1.0f);
     float sin_theta = sqrtf(1.0f - cos_theta * cos_theta);
@@ -818,17 +853,16 @@ HRT_LANE_FI bool shade(const KParams& P, PathState& ps, uint32_t winner, float c
     else ndir = refract(ud, rec.n, ratio);
     att = v3(1.0f, 1.0f, 1.0f);
     scattered = true;
-  } else if (FULL && M.kind == G::M_DIFFUSE_LIGHT) { /* diffuse_light.rs:20-28 */
+  } else if (FULL && kind == G::M_DIFFUSE_LIGHT) { /* diffuse_light.rs:20-28 */
     textured = true;
-  } else if (FULL && M.kind == G::M_ISOTROPIC) { /* isotropic.rs:26-33 */
+  } else if (FULL && kind == G::M_ISOTROPIC) { /* isotropic.rs:26-33 */
     ndir = sph;
     textured = true;
     scattered = true;
   }
-  /* textures draw no random numbers, so one evaluation after the scatter keeps the draw order */
   if (textured) {
-    const Vec3 tv = tex_value<FULL, COUNT>(P, M.tex, rec.u, rec.v, rec.p, cn);
-    if (FULL && M.kind == G::M_DIFFUSE_LIGHT) emitted = tv;
+    const Vec3 tv = tex();
+    if (FULL && kind == G::M_DIFFUSE_LIGHT) emitted = tv;
     else att = tv;
   }
   /* L = emitted + att * L_next, accumulated front to back */
@@ -839,6 +873,65 @@ HRT_LANE_FI bool shade(const KParams& P, PathState& ps, uint32_t winner, float c
   ps.rd = ndir;
   ps.depth_left--;
   return false;
+}
+
+/* The part of one ray_color step after world.hit (application.rs:483-494): background on a miss,
+ * else hit record, emission and scatter.  (ro, rd, rtime) is the segment just traced; the scattered
+ * ray goes to ps.ro/ps.rd.  Returns true when the path is finished. */
+template <bool FULL, bool COUNT>
+HRT_LANE_FI bool shade(const KParams& P, PathState& ps, uint32_t winner, float closest, Vec3 ro,
+                                      Vec3 rd, float rtime, float tau, Counts& cn) {
+  if (winner == G::NONE) {
+    ps.rad = ps.rad + mul_elem(ps.thr, P.background);
+    return true;
+  }
+  const Rec rec = make_record<FULL>(P, winner, closest, ro, rd, rtime, tau);
+  const G::Mat M = P.mats[rec.mat];
+  return scatter<FULL>(ps, rec, M.kind, v3(M.a[0], M.a[1], M.a[2]), M.a[3], M.a[0], rd,
+                       [&]() { return tex_value<FULL, COUNT>(P, M.tex, rec.u, rec.v, rec.p, cn); });
+}
+
+/* shade() for the sphere kernel's walk stream: the winner is a leaf record (layout.h), which holds the
+ * sphere and its material, so the hit record and the scatter read the walk stream only (LDS). */
+template <bool COUNT, int MEM>
+HRT_LANE_FI bool shade_walk(const KParams& P, const WalkSrc& src, PathState& ps, uint32_t leaf, float closest,
+                            Vec3 ro, Vec3 rd, float rtime, float tau, Counts& cn) {
+  if (leaf == G::NONE) {
+    ps.rad = ps.rad + mul_elem(ps.thr, P.background);
+    return true;
+  }
+  /* sphere.rs:57-73 / moving_sphere.rs:80-94 */
+  const float4 bmn = wload<MEM>(src, leaf + 32u), bmx = wload<MEM>(src, leaf + 48u);
+  const float4 s0 = wload<MEM>(src, leaf + 64u);
+  Vec3 c = v3(s0.x, s0.y, s0.z);
+  if (f2u(bmn.w) & G::WL_MOVING) {
+    const float4 s1 = wload<MEM>(src, leaf + 80u);
+    const float f = P.motion_uniform ? tau : (rtime - s0.w) / s1.w;
+    c = c + f * v3(s1.x, s1.y, s1.z);
+  }
+  Rec rec;
+  rec.u = 0.0f;
+  rec.v = 0.0f;
+  const Vec3 at = ro + closest * rd;
+  const Vec3 outward = (at - c) / bmx.w;
+  rec.p = at;
+  set_face_normal(rec, rd, outward);
+  const float4 ma = wload<MEM>(src, leaf + 96u), mb = wload<MEM>(src, leaf + 112u);
+  const uint32_t mw = f2u(mb.w);
+  rec.mat = mw >> 8;
+  const uint32_t wt = (mw >> 4) & 15u;
+  return scatter<false>(ps, rec, mw & 15u, v3(ma.x, ma.y, ma.z), ma.w, ma.w, rd, [&]() {
+    if (wt == G::WT_SOLID) {
+      if constexpr (COUNT) cn.tex++;
+      return v3(ma.x, ma.y, ma.z);
+    }
+    if (wt == G::WT_CHECKER) { /* checker_texture.rs:22-29 over two SolidColors */
+      if constexpr (COUNT) cn.tex += 2;
+      return checker_odd(10.0f * rec.p.x, 10.0f * rec.p.y, 10.0f * rec.p.z) ? v3(ma.x, ma.y, ma.z)
+                                                                             : v3(mb.x, mb.y, mb.z);
+    }
+    return tex_value<false, COUNT>(P, P.mats[rec.mat].tex, rec.u, rec.v, rec.p, cn);
+  });
 }
 
 /* One step of ray_color (application.rs:477-495).  Returns true when the path is finished.
@@ -968,34 +1061,6 @@ HRT_LANE_FI void basic_step(const KParams& P, const G::Node* __restrict__ nodes,
   if (walk_pending(i)) basic_prim<CULL, COUNT>(P, nodes, prims, i, r, closest, winner, cn);
 }
 
-/* ------------------------------------------------------------------ the sphere-scene walk stream */
-/* The walk of render_basic_kernel under CULL_EXACT, over the walk stream (layout.h): positions are
- * byte offsets, read from LDS (the stream staged at LDS address 0), from global memory through a buffer
- * descriptor (32-bit offsets, no 64-bit address arithmetic per step), or from a host pointer (the lane
- * simulator). */
-enum : int { WM_LDS = 0, WM_BUF = 1, WM_HOST = 2 };
-struct WalkSrc {
-  const uint8_t* base; /* WM_BUF: the section in global memory; WM_HOST: the host copy */
-#if defined(__HIP_DEVICE_COMPILE__)
-  __amdgpu_buffer_rsrc_t rsrc; /* WM_BUF */
-#endif
-};
-
-template <int MEM>
-HRT_LANE_FI float4 wload(const WalkSrc& src, uint32_t off) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  if constexpr (MEM == WM_LDS) {
-    typedef __attribute__((address_space(3))) const float4 lds_float4;
-    return *(const lds_float4*)(size_t)off;
-  } else if constexpr (MEM == WM_BUF) {
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    const f4v v = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(src.rsrc, (int)off, 0, 0));
-    return make_float4(v.x, v.y, v.z, v.w);
-  }
-#endif
-  return *reinterpret_cast<const float4*>(src.base + off);
-}
-
 /* The inflated test of CULL_EXACT on a box given by centre C and half-extent E (the walk stream's inner
  * boxes, which hold the reference boxes): false only if the box, widened by EXACT_MARGIN x D' (D' =
  * max_k |C_k - o_k| + E_k >= the L-inf distance of its farthest point from the origin), misses the ray
@@ -1062,7 +1127,7 @@ HRT_LANE_FI void walk_prim(const KParams& P, const WalkSrc& src, uint32_t& i, co
   float t;
   if (sphere_root_at(c, bmx.w, r, P.t_min, closest, t)) {
     closest = t;
-    winner = w >> 2;
+    winner = leaf; /* shade_walk reads the sphere and its material from the leaf */
   }
 }
 

@@ -150,19 +150,28 @@ constexpr uint32_t KIND_MASK = 0x7Fu;
  * boxes contain their leaves' boxes gives the same result: the inflated test is conservative for any
  * box that holds the geometry, and the reference test is applied at leaves).
  *   inner (32 B): float4(C.xyz, skip)  float4(E.xyz, pass)
- *   leaf  (96 B): float4(C.xyz, skip)  float4(E.xyz, pass)
+ *   leaf (128 B): float4(C.xyz, skip)  float4(E.xyz, pass)
  *                 float4(mn.xyz, w)    float4(mx.xyz, radius)      the reference box (aabb.rs test)
  *                 float4(c0.xyz, t0)   float4(c1 - c0, t1 - t0)    the sphere (moving_sphere.rs:55-58)
+ *                 float4(A.xyz, f)     float4(B.xyz, mw)           its material, inline (shading reads no
+ *                                                                  global memory): mw = M_* kind |
+ *                                                                  WT_* << 4 | material index << 8;
+ *                                                                  A = albedo (WT_SOLID, Metal) or the
+ *                                                                  checker's odd colour, B its even
+ *                                                                  colour (WT_CHECKER), f = fuzz (Metal)
+ *                                                                  or ior (Dielectric); WT_GLOBAL: the
+ *                                                                  texture is read from texs (any tree)
  * C, E: centre and half-extent of a box holding the node's box ([C - E, C + E] contains [mn, mx] in
  * real arithmetic: E rounded up), for the inflated test (lane.h box_ce).  skip = byte offset one past
  * the subtree; pass = offset of the next node for an inner node, and (self | WALK_PEND) for a leaf: the
  * lane parks on the leaf until the wave runs its primitive test (walk_prim), which continues at
- * self + WALK_LEAF_BYTES.  w = WL_* flags | primitive index << 2 (the index of the prims section, the
- * walk's winner).  A leaf without a reference box (a List member: K_PRIM) has C = 0, E = +inf (the
+ * self + WALK_LEAF_BYTES.  w = WL_* flags | primitive index << 2 (the index of the prims section); the
+ * walk's winner is the leaf's offset.  A leaf without a reference box (a List member: K_PRIM) has C = 0, E = +inf (the
  * inflated test always passes) and WL_NOBOX (no reference test). */
 constexpr uint32_t WALK_PEND = 1u << 31;
-constexpr uint32_t WALK_INNER_BYTES = 32, WALK_LEAF_BYTES = 96;
+constexpr uint32_t WALK_INNER_BYTES = 32, WALK_LEAF_BYTES = 128;
 constexpr uint32_t WL_MOVING = 1u, WL_NOBOX = 2u;
+enum : uint32_t { WT_SOLID = 0, WT_CHECKER = 1, WT_GLOBAL = 2 }; /* inline texture of a leaf's material */
 
 }  // namespace gpu
 }  // namespace hrt

@@ -392,8 +392,12 @@ void render_basic_kernel(KParams P) {
     const bool traced = shading && node != G::NONE;
     bool sample_done = false, chunk_done = false;
     if (shading) {
-      const bool done =
-          !traced || shade<false, COUNT>(P, ps, winner, closest, r.o, r.d, r.time, r.tau, cn) || ps.depth_left == 0;
+      bool done = true;
+      if (traced) {
+        if constexpr (WS) done = shade_walk<COUNT, WMEM>(P, ws, ps, winner, closest, r.o, r.d, r.time, r.tau, cn);
+        else done = shade<false, COUNT>(P, ps, winner, closest, r.o, r.d, r.time, r.tau, cn);
+        done = done || ps.depth_left == 0;
+      }
       if (done) {
         /* application.rs:448: samples of a chunk summed in order */
         walking = false;
@@ -695,9 +699,10 @@ void launch_basic(const KParams& kp, int device, hipStream_t stream, size_t smem
   hip_check(hipGetLastError(), "render_basic_kernel launch");
 }
 
-/* LDS residency: the reference-order stream must fit twice per CU (two 512-thread workgroups of the
- * 160 KiB), the 8 SAH octant streams once (one 1024-thread workgroup). */
-constexpr size_t LDS_SCENE_MAX = 72 * 1024;
+/* LDS residency: the scene a sphere-kernel workgroup stages (the walk stream, or the reference-order
+ * stream) must fit twice per CU (two workgroups of the 160 KiB), the 8 SAH octant streams once (one
+ * 1024-thread workgroup). */
+constexpr size_t LDS_SCENE_MAX = 78 * 1024;
 constexpr size_t LDS_FAST_MAX = 150 * 1024;
 constexpr size_t LDS_GEN_MAX = 48 * 1024;
 

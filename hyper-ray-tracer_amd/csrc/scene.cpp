@@ -565,6 +565,8 @@ void box_ce_of(const Vec3& mn, const Vec3& mx, float* C, float* E) {
 struct WalkBuilder {
   hrt_scene* s;
   std::vector<float>& out;
+  uint32_t inner_bytes; /* 32, or 48 (HRT_WALK_INNER=48: a zero pad spreading records over the LDS bank
+                         * slots; measured 0.8% slower, so not the default) */
   uint32_t words() const { return (uint32_t)out.size(); }
   uint32_t bytes() const { return 4u * words(); }
   static void put4(std::vector<float>& o, float a, float b, float c, float d) {
@@ -575,7 +577,8 @@ struct WalkBuilder {
     box_ce_of(box.mn, box.mx, C, E);
     const uint32_t self = bytes();
     put4(out, C[0], C[1], C[2], u2f(skip));
-    put4(out, E[0], E[1], E[2], u2f(self + G::WALK_INNER_BYTES));
+    put4(out, E[0], E[1], E[2], u2f(self + inner_bytes));
+    for (uint32_t k = G::WALK_INNER_BYTES; k < inner_bytes; k += 16) put4(out, 0.0f, 0.0f, 0.0f, 0.0f);
   }
   void leaf(const WalkLeaf& L) {
     const uint32_t self = bytes();
@@ -593,11 +596,37 @@ struct WalkBuilder {
     put4(out, L.box.mx.x, L.box.mx.y, L.box.mx.z, p.p0[3]);
     put4(out, p.p0[0], p.p0[1], p.p0[2], moving ? p.p1[3] : 0.0f);
     put4(out, moving ? p.p1[0] : 0.0f, moving ? p.p1[1] : 0.0f, moving ? p.p1[2] : 0.0f, moving ? p.p2[0] : 1.0f);
+    /* the material, inline (layout.h) */
+    const uint32_t mi = p.km >> 4;
+    need(mi < (1u << 24), HRT_ERR_UNSUPPORTED, "too many materials for the walk stream");
+    const G::Mat& m = s->g_mats[mi];
+    float A[4] = {0.0f, 0.0f, 0.0f, 0.0f}, Bc[3] = {0.0f, 0.0f, 0.0f};
+    uint32_t wt = G::WT_GLOBAL;
+    if (m.kind == G::M_METAL) {
+      A[0] = m.a[0]; A[1] = m.a[1]; A[2] = m.a[2]; A[3] = m.a[3];
+      wt = G::WT_SOLID;
+    } else if (m.kind == G::M_DIELECTRIC) {
+      A[3] = m.a[0];
+      wt = G::WT_SOLID;
+    } else {
+      const G::Tex& t = s->g_texs[m.tex];
+      if (t.kind == G::T_SOLID) {
+        A[0] = t.a[0]; A[1] = t.a[1]; A[2] = t.a[2];
+        wt = G::WT_SOLID;
+      } else if (t.kind == G::T_CHECKER && s->g_texs[t.i0].kind == G::T_SOLID && s->g_texs[t.i1].kind == G::T_SOLID) {
+        const G::Tex &odd = s->g_texs[t.i0], &even = s->g_texs[t.i1];
+        A[0] = odd.a[0]; A[1] = odd.a[1]; A[2] = odd.a[2];
+        Bc[0] = even.a[0]; Bc[1] = even.a[1]; Bc[2] = even.a[2];
+        wt = G::WT_CHECKER;
+      }
+    }
+    put4(out, A[0], A[1], A[2], A[3]);
+    put4(out, Bc[0], Bc[1], Bc[2], u2f(m.kind | wt << 4 | mi << 8));
   }
 };
 
-uint32_t walk_subtree_bytes(uint32_t n_leaves) {
-  return (n_leaves - 1) * G::WALK_INNER_BYTES + n_leaves * G::WALK_LEAF_BYTES;
+uint32_t walk_subtree_bytes(uint32_t n_leaves, uint32_t inner_bytes) {
+  return (n_leaves - 1) * inner_bytes + n_leaves * G::WALK_LEAF_BYTES;
 }
 
 double half_area(const Aabb& b) {
@@ -644,7 +673,7 @@ void walk_regroup(WalkBuilder& B, const std::vector<WalkLeaf>& leaves) {
         best = k;
       }
     }
-    B.inner(pre[n - 1], B.bytes() + walk_subtree_bytes(n));
+    B.inner(pre[n - 1], B.bytes() + walk_subtree_bytes(n, B.inner_bytes));
     todo.push_back({r.lo + best + 1, r.hi}); /* right after left */
     todo.push_back({r.lo, r.lo + best + 1});
   }
@@ -676,7 +705,8 @@ void build_walk(hrt_scene* s) {
   if (leaves.empty()) return;
   const char* mode = getenv("HRT_WALK_TREE");
   const bool regroup = regroup_ok && !(mode && strcmp(mode, "reference") == 0);
-  WalkBuilder B{s, s->w_stream};
+  const char* pad = getenv("HRT_WALK_INNER");
+  WalkBuilder B{s, s->w_stream, pad && strcmp(pad, "48") == 0 ? 48u : G::WALK_INNER_BYTES};
   if (regroup) {
     walk_regroup(B, leaves);
     s->w_regrouped = true;
@@ -685,7 +715,7 @@ void build_walk(hrt_scene* s) {
     uint32_t off = 0;
     for (uint32_t i = 0; i < n; i++) {
       at[i] = off;
-      off += ((s->g_nodes[i].kp >> 24) & G::KIND_MASK) == G::K_BOX ? G::WALK_INNER_BYTES : G::WALK_LEAF_BYTES;
+      off += ((s->g_nodes[i].kp >> 24) & G::KIND_MASK) == G::K_BOX ? B.inner_bytes : G::WALK_LEAF_BYTES;
     }
     at[n] = off;
     size_t li = 0;
@@ -703,7 +733,8 @@ void build_walk(hrt_scene* s) {
     }
   }
   s->w_end = B.bytes();
-  need(s->w_end == walk_subtree_bytes((uint32_t)leaves.size()) || !regroup, HRT_ERR_STATE, "walk stream size");
+  need(s->w_end == walk_subtree_bytes((uint32_t)leaves.size(), B.inner_bytes) || !regroup, HRT_ERR_STATE,
+       "walk stream size");
 }
 
 void flatten(hrt_scene* s) {

@@ -404,6 +404,9 @@ HRT_HD float gen_signed_unit(Rng& r) {
 
 /* math.rs:16-30 random_in_unit_sphere: rejection on Uniform(-1,1)^3 */
 HRT_HD Vec3 random_in_unit_sphere(Rng& r) {
+#if HRT_EXP_NOREJECT /* timing experiment only (wrong draws): the price of the rejection loops */
+  { float x = gen_signed_unit(r), y = gen_signed_unit(r), z = gen_signed_unit(r); return v3(0.5f * x, 0.5f * y, 0.5f * z); }
+#endif
   for (;;) {
     float x = gen_signed_unit(r);
     float y = gen_signed_unit(r);
@@ -416,6 +419,9 @@ HRT_HD Vec3 random_in_unit_sphere(Rng& r) {
 HRT_HD Vec3 random_unit_vector(Rng& r) { return normalize(random_in_unit_sphere(r)); }
 /* math.rs:32-40 */
 HRT_HD Vec3 random_in_unit_disk(Rng& r) {
+#if HRT_EXP_NOREJECT
+  { float x = gen_signed_unit(r), y = gen_signed_unit(r); return v3(0.5f * x, 0.5f * y, 0.0f); }
+#endif
   for (;;) {
     float x = gen_signed_unit(r);
     float y = gen_signed_unit(r);

@@ -74,8 +74,15 @@ void render_pixel(const KParams& P, uint32_t px, uint32_t py, float* rgba, uint6
             while (node < P.main_end) basic_step<CULL, true>(P, P.nodes, P.prims, node, r, closest, winner, cn);
           }
           traced = node != G::NONE;
-          done = !traced ||
-                 shade<false, true>(P, ps, winner, closest, r.o, r.d, r.time, r.tau, cn) || ps.depth_left == 0;
+          if constexpr (CULL == G::CULL_EXACT) {
+            WalkSrc src;
+            src.base = P.walk;
+            done = !traced || shade_walk<true, WM_HOST>(P, src, ps, winner, closest, r.o, r.d, r.time, r.tau, cn) ||
+                   ps.depth_left == 0;
+          } else {
+            done = !traced ||
+                   shade<false, true>(P, ps, winner, closest, r.o, r.d, r.time, r.tau, cn) || ps.depth_left == 0;
+          }
         }
         if (traced) cnt[0]++;
         if (done) break;
