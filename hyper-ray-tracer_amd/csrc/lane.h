@@ -975,10 +975,8 @@ HRT_LANE_FI void init_path_state(PathState& ps) {
  * `pend` (its index).  basic_prim then tests it against the lane's current `closest`.  A lane runs
  * basic_prim before its next basic_box, so its sequence of tests is exactly basic_step's; the kernel
  * only chooses WHEN, batching the primitive tests of many lanes into one execution of the divergent
- * sphere block.
- * Under CULL_EXACT, basic_box applies the inflated test alone and basic_prim applies the reference
- * test to the leaf's box first (box_ref: the reference test is monotone, so leaves suffice); the
- * other modes test the whole box in basic_box. */
+ * sphere block.  These walk the reference node stream under CULL_REFERENCE / CULL_SLAB (the
+ * verbatim-reference and approximate modes); CULL_EXACT walks the walk stream (walk_box / walk_prim). */
 /* The walk position of the BASIC kernel is ONE register: the next node's index, with WALK_PEND set
  * while the primitive of the leaf just passed (index - 1) waits for its test, or NONE when the lane
  * has no walk.  So "can step" is the single compare i < end, and the waiting primitive is read back
@@ -986,9 +984,6 @@ HRT_LANE_FI void init_path_state(PathState& ps) {
 constexpr uint32_t WALK_PEND = G::WALK_PEND;
 HRT_LANE_FI bool walk_pending(uint32_t i) { return i - WALK_PEND < 0x7FFFFFFFu; } /* PEND set, i != NONE */
 
-/* A BASIC scene holds K_BOX, K_BOX_PRIM and K_PRIM nodes only (F_BASIC: no instances or media), so
- * kp >= K_PRIM << 24 holds exactly for the nodes the inflated test must pass: K_PRIM (no box) and
- * NODE_REF_ONLY (bit 31). */
 /* STRIDE: the walk position is a node index (1), or the node's LDS byte address (32, sizeof(Node)):
  * the LDS-resident stream is staged with its skip links turned into LDS addresses, so a step loads
  * its node straight from the position, with no address arithmetic. */
@@ -1021,11 +1016,8 @@ HRT_LANE_FI void basic_box(const KParams& P, const G::Node* __restrict__ nodes, 
 #endif
   const uint32_t kp = f2u(b.w);
   if constexpr (COUNT) cn.nodes++;
-  bool pass;
-  if constexpr (CULL == G::CULL_EXACT)
-    pass = box_infl(a, b, r, P.t_min, closest) || kp >= (G::K_PRIM << 24);
-  else
-    pass = box_hit<CULL>(a, b, r, P.t_min, closest) || ((kp >> 24) & G::KIND_MASK) == G::K_PRIM;
+  static_assert(CULL != G::CULL_EXACT, "CULL_EXACT walks the walk stream (walk_box)");
+  const bool pass = box_hit<CULL>(a, b, r, P.t_min, closest) || ((kp >> 24) & G::KIND_MASK) == G::K_PRIM;
   const bool prim = (kp & (G::KIND_MASK << 24)) != 0u; /* K_BOX_PRIM or K_PRIM: a primitive to test */
   const uint32_t next = i + (prim ? STRIDE + WALK_PEND : STRIDE);
   i = pass ? next : skip;
@@ -1039,9 +1031,6 @@ HRT_LANE_FI void basic_prim(const KParams& P, const G::Node* __restrict__ nodes,
   float4 a, b;
   load_node<STRIDE>(nodes, i - STRIDE, a, b);
   const uint32_t kp = f2u(b.w);
-  if constexpr (CULL == G::CULL_EXACT) {
-    if (((kp >> 24) & G::KIND_MASK) != G::K_PRIM && !box_ref(a, b, r, P.t_min, closest)) return;
-  }
   const uint32_t payload = kp & 0xFFFFFFu;
   const G::Prim* pp = prims + payload;
   if constexpr (COUNT) cn.prims++;

@@ -169,6 +169,8 @@ constexpr uint32_t KIND_MASK = 0x7Fu;
  * walk's winner is the leaf's offset.  A leaf without a reference box (a List member: K_PRIM) has C = 0, E = +inf (the
  * inflated test always passes) and WL_NOBOX (no reference test). */
 constexpr uint32_t WALK_PEND = 1u << 31;
+/* the largest scene a sphere-kernel workgroup stages in LDS: two workgroups per CU share its 160 KiB */
+constexpr uint32_t LDS_SCENE_MAX_BYTES = 78u * 1024u;
 constexpr uint32_t WALK_INNER_BYTES = 32, WALK_LEAF_BYTES = 128;
 constexpr uint32_t WL_MOVING = 1u, WL_NOBOX = 2u;
 enum : uint32_t { WT_SOLID = 0, WT_CHECKER = 1, WT_GLOBAL = 2 }; /* inline texture of a leaf's material */

@@ -702,7 +702,7 @@ void launch_basic(const KParams& kp, int device, hipStream_t stream, size_t smem
 /* LDS residency: the scene a sphere-kernel workgroup stages (the walk stream, or the reference-order
  * stream) must fit twice per CU (two workgroups of the 160 KiB), the 8 SAH octant streams once (one
  * 1024-thread workgroup). */
-constexpr size_t LDS_SCENE_MAX = 78 * 1024;
+constexpr size_t LDS_SCENE_MAX = G::LDS_SCENE_MAX_BYTES;
 constexpr size_t LDS_FAST_MAX = 150 * 1024;
 constexpr size_t LDS_GEN_MAX = 48 * 1024;
 

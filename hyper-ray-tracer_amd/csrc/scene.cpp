@@ -1221,12 +1221,10 @@ hrt_status hrt_scene_get_info(const hrt_scene* s, hrt_scene_info* info) {
     info->media = (uint32_t)s->g_media.size();
     info->feature_mask = s->feature_mask;
     info->blob_bytes = (uint32_t)s->blob_bytes;
-    info->in_lds = ((s->feature_mask & ~G::F_BASIC) == 0 &&
-                    s->main_end * sizeof(G::Node) + s->g_prims.size() * sizeof(G::Prim) <= 72 * 1024) ? 1u : 0u;
+    /* the default plan (render.hip plan()): sphere scenes stage their walk stream in LDS when it fits */
+    info->in_lds = ((s->feature_mask & ~G::F_BASIC) == 0 && s->w_end > 0 && s->w_end <= G::LDS_SCENE_MAX_BYTES) ? 1u : 0u;
     info->cull_mode = (uint32_t)s->cull_mode;
     info->sah_stream_len = s->f_stream_len;
-    if (s->f_stream_len) /* the plan the renderer uses for a [0,1] shutter (render.hip plan()) */
-      info->in_lds = 8 * s->f_stream_len * sizeof(G::Node) + s->f_prims.size() * sizeof(G::Prim) <= 150 * 1024 ? 1u : 0u;
   });
 }
 
