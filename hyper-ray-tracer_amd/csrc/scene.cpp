@@ -198,6 +198,23 @@ uint32_t build_bvh(hrt_scene* s, std::vector<uint32_t> objects, float t0, float 
                    [](const std::pair<float, uint32_t>& a, const std::pair<float, uint32_t>& b) {
                      return a.first < b.first;
                    });
+  /* HRT_BVH_TIES=reverse (diagnostics): sorts of more than 20 objects put equal keys in the reverse
+   * order, another order Rust's pdqsort could produce; tests/test_gpu_configs.py renders both trees to
+   * show what the unpinned tie order changes (hrt_scene_info.bvh_tied_sorts) */
+  const char* ties = getenv("HRT_BVH_TIES");
+  if (ties && strcmp(ties, "reverse") == 0 && keys.size() > 20)
+    for (size_t i = 0; i < keys.size();) {
+      size_t j = i + 1;
+      while (j < keys.size() && keys[j].first == keys[i].first) j++;
+      std::reverse(keys.begin() + i, keys.begin() + j);
+      i = j;
+    }
+  if (keys.size() > 20)
+    for (size_t i = 1; i < keys.size(); i++)
+      if (keys[i].first == keys[i - 1].first) {
+        s->bvh_tied_sorts++;
+        break;
+      }
   HNode n;
   n.kind = N_BVH;
   n.has_box = true;
@@ -1225,6 +1242,8 @@ hrt_status hrt_scene_get_info(const hrt_scene* s, hrt_scene_info* info) {
     info->in_lds = ((s->feature_mask & ~G::F_BASIC) == 0 && s->w_end > 0 && s->w_end <= G::LDS_SCENE_MAX_BYTES) ? 1u : 0u;
     info->cull_mode = (uint32_t)s->cull_mode;
     info->sah_stream_len = s->f_stream_len;
+    info->bvh_tied_sorts = s->bvh_tied_sorts;
+    info->walk_regrouped = s->w_regrouped ? 1u : 0u;
   });
 }
 
@@ -1260,6 +1279,7 @@ hrt_status hrt_debug_scene_blob(hrt_scene* s, void* out, uint64_t cap, uint64_t*
       info->off_walk = s->off_walk;
       info->walk_bytes = s->w_end;
       info->walk_regrouped = s->w_regrouped ? 1u : 0u;
+      info->bvh_tied_sorts = s->bvh_tied_sorts;
     }
   });
 }

@@ -73,6 +73,7 @@ struct hrt_scene {
   std::vector<hrt::gpu::Perlin> perlin;
   std::vector<uint8_t> images;
   uint32_t root = hrt::gpu::NONE;
+  uint32_t bvh_tied_sorts = 0; /* BvhNode::new sorts of > 20 objects with equal keys (hrt_scene_info) */
   uint32_t n_media = 0;
   bool committed = false;
 

@@ -103,7 +103,8 @@ class BlobInfo(ctypes.Structure):
         [(n, ctypes.c_uint32) for n in ("n_nodes", "main_end", "n_prims", "feature_mask", "cull_mode", "motion_uniform")] + \
         [("motion_t0", ctypes.c_float), ("motion_span", ctypes.c_float), ("ln_e", ctypes.c_float),
          ("media_nested", ctypes.c_uint32), ("box_t0", ctypes.c_float), ("box_t1", ctypes.c_float),
-         ("off_walk", ctypes.c_uint64), ("walk_bytes", ctypes.c_uint32), ("walk_regrouped", ctypes.c_uint32)]
+         ("off_walk", ctypes.c_uint64), ("walk_bytes", ctypes.c_uint32), ("walk_regrouped", ctypes.c_uint32),
+         ("bvh_tied_sorts", ctypes.c_uint32)]
 
 
 class PresetInfo(ctypes.Structure):
@@ -123,7 +124,8 @@ class PresetInfo(ctypes.Structure):
 class SceneInfo(ctypes.Structure):
     _fields_ = [
         (n, ctypes.c_uint32)
-        for n in ("nodes", "prims", "materials", "textures", "instances", "media", "feature_mask", "blob_bytes", "in_lds", "cull_mode", "sah_stream_len")
+        for n in ("nodes", "prims", "materials", "textures", "instances", "media", "feature_mask", "blob_bytes", "in_lds",
+                  "cull_mode", "sah_stream_len", "bvh_tied_sorts", "walk_regrouped")
     ]
 
 

@@ -264,6 +264,11 @@ typedef struct hrt_scene_info {
   uint32_t in_lds;         /* 1 if the megakernel stages the scene in LDS */
   uint32_t cull_mode;      /* default culling: 2 = exact (reference test + provably safe extra culling) */
   uint32_t sah_stream_len; /* >0: sphere-only scene with the SAH octant streams (8 x this many nodes) */
+  /* BvhNode::new sorts of more than 20 objects with equal keys (bvh_node.rs:34): Rust's sort_unstable_by
+   * may order such ties differently from this build's stable sort (below 21 objects both are an
+   * insertion sort), so 0 means the BVH topology is the reference's for any Rust version */
+  uint32_t bvh_tied_sorts;
+  uint32_t walk_regrouped; /* sphere scenes: the walk stream's inner boxes are re-grouped (layout.h) */
 } hrt_scene_info;
 hrt_status hrt_scene_get_info(const hrt_scene* s, hrt_scene_info* info);
 /* Write an RGBA f32 frame (w x h, row-major, row 0 = image y 0 = bottom, as the render calls produce;
@@ -294,6 +299,7 @@ typedef struct hrt_blob_info {
   uint64_t off_walk;       /* sphere scenes: the walk stream of the default (exact) sphere kernel */
   uint32_t walk_bytes;     /* its size (0: not a sphere scene) */
   uint32_t walk_regrouped; /* its inner boxes re-grouped over the reference leaf order */
+  uint32_t bvh_tied_sorts; /* as hrt_scene_info */
 } hrt_blob_info;
 hrt_status hrt_debug_scene_blob(hrt_scene* s, void* out, uint64_t cap, uint64_t* size, hrt_blob_info* info);
 /* Overwrite n bytes of the committed scene's DEVICE blob at byte `offset` (hrt_blob_info offsets), after
