@@ -357,6 +357,17 @@ HRT_LANE_FI bool sphere_root(const G::Prim* pp, uint32_t kind, const TRay& r, fl
   return sphere_root_at(c, p0.w, r, tmin, tmax, root);
 }
 
+/* Component i of v, and v with components a and b replaced, by selects: writing through Vec3's
+ * runtime-indexed operator[] (a reference to a member chosen at run time) puts the vector in scratch
+ * memory on the GPU, which in the walk loop cost more than all its arithmetic. */
+HRT_LANE_FI float comp(const Vec3& v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
+HRT_LANE_FI Vec3 with2(Vec3 v, int a, float va, int b, float vb) {
+  v.x = a == 0 ? va : (b == 0 ? vb : v.x);
+  v.y = a == 1 ? va : (b == 1 ? vb : v.y);
+  v.z = a == 2 ? va : (b == 2 ? vb : v.z);
+  return v;
+}
+
 HRT_LANE_FI void plane_axes(uint32_t plane, int& k, int& a, int& b) {
   /* rect.rs:55-59 */
   if (plane == HRT_PLANE_XY) { k = 2; a = 0; b = 1; }
@@ -371,10 +382,10 @@ HRT_LANE_FI bool rect_t(const G::Prim* pp, uint32_t plane, const TRay& r, float 
   plane_axes(plane, k, a, b);
   float4 p0 = ld4(pp->p0);
   float kk = pp->p1[0];
-  float t = (kk - r.o[k]) / r.d[k];
+  float t = (kk - comp(r.o, k)) / comp(r.d, k);
   if (t < tmin || t > tmax) return false;
-  float av = r.o[a] + t * r.d[a];
-  float bv = r.o[b] + t * r.d[b];
+  float av = comp(r.o, a) + t * comp(r.d, a);
+  float bv = comp(r.o, b) + t * comp(r.d, b);
   if (av < p0.x || av > p0.y || bv < p0.z || bv > p0.w) return false;
   tout = t;
   return true;
@@ -382,19 +393,15 @@ HRT_LANE_FI bool rect_t(const G::Prim* pp, uint32_t plane, const TRay& r, float 
 
 /* translation.rs:26-30 and rotation.rs:104-117: the ray handed to the child */
 HRT_LANE_FI void inst_ray(const G::Inst& in, Vec3& o, Vec3& d) {
-  if (in.kind == G::I_TRANSLATE) {
+  if ((in.kind & G::I_KIND_MASK) == G::I_TRANSLATE) {
     o = o - v3(in.d[0], in.d[1], in.d[2]);
     return;
   }
   int a = (int)(in.axis + 1) % 3, b = (int)(in.axis + 2) % 3;
   float s = in.sin_t, c = in.cos_t;
-  Vec3 no = o, nd = d;
-  no[a] = c * o[a] + s * o[b];
-  no[b] = -s * o[a] + c * o[b];
-  nd[a] = c * d[a] + s * d[b];
-  nd[b] = -s * d[a] + c * d[b];
-  o = no;
-  d = nd;
+  const float oa = comp(o, a), ob = comp(o, b), da = comp(d, a), db = comp(d, b);
+  o = with2(o, a, c * oa + s * ob, b, -s * oa + c * ob);
+  d = with2(d, a, c * da + s * db, b, -s * da + c * db);
 }
 
 /* The ray in the frame of instance q's children: the world ray through q's enclosing chain, outermost
@@ -407,6 +414,45 @@ HRT_LANE_FI void apply_chain(const KParams& P, uint32_t q, Vec3& o, Vec3& d) {
     uint32_t x = q;
     for (int s = 0; s < l; s++) x = P.insts[x].parent;
     inst_ray(P.insts[x], o, d);
+  }
+}
+
+/* The walk enters instance `in` (K_INST_BEGIN): the ray of its children's frame.  set_dir's derived
+ * fields are recomputed only when the frame changes them and the subtree reads them (layout.h IF_*):
+ * a Translation keeps d, so 1/d and d.d stay; a Rotation whose subtree holds only rects needs none of
+ * them.  Fields left alone keep the enclosing frame's values, which every instance below restores on
+ * its way out, so they are right again when the walk leaves this instance. */
+HRT_LANE_FI void inst_enter(const G::Inst& in, TRay& r) {
+  Vec3 no = r.o, nd = r.d;
+  inst_ray(in, no, nd);
+  r.o = no;
+  if ((in.kind & G::I_KIND_MASK) == G::I_TRANSLATE) return;
+  r.d = nd;
+  if (in.kind & G::IF_INV) {
+    r.inv = v3(1.0f / nd.x, 1.0f / nd.y, 1.0f / nd.z);
+    r.minv = v3(G::EXACT_MARGIN * fabsf(r.inv.x), G::EXACT_MARGIN * fabsf(r.inv.y), G::EXACT_MARGIN * fabsf(r.inv.z));
+  }
+  if (in.kind & G::IF_DD) {
+    r.dd = dot(nd, nd);
+    r.rdd = div_rn_y(r.dd);
+  }
+}
+
+/* ... and leaves it (K_INST_END): the enclosing frame's ray, re-derived from the walk's starting ray
+ * (base_o, base_d) through the enclosing chain, and what inst_enter changed recomputed. */
+HRT_LANE_FI void inst_leave(const KParams& P, const G::Inst& in, TRay& r, Vec3 base_o, Vec3 base_d) {
+  Vec3 no = base_o, nd = base_d;
+  apply_chain(P, in.parent, no, nd);
+  r.o = no;
+  if ((in.kind & G::I_KIND_MASK) == G::I_TRANSLATE) return;
+  r.d = nd;
+  if (in.kind & G::IF_INV) {
+    r.inv = v3(1.0f / nd.x, 1.0f / nd.y, 1.0f / nd.z);
+    r.minv = v3(G::EXACT_MARGIN * fabsf(r.inv.x), G::EXACT_MARGIN * fabsf(r.inv.y), G::EXACT_MARGIN * fabsf(r.inv.z));
+  }
+  if (in.kind & G::IF_DD) {
+    r.dd = dot(nd, nd);
+    r.rdd = div_rn_y(r.dd);
   }
 }
 
@@ -476,13 +522,9 @@ HRT_LANE void trace(const KParams& P, const G::Node* __restrict__ nodes, const G
       if constexpr (FULL) {
         i++;
         if (kind == G::K_INST_BEGIN) {
-          Vec3 no = r.o, nd = r.d;
-          inst_ray(P.insts[payload], no, nd);
-          set_dir(r, no, nd);
+          inst_enter(P.insts[payload], r);
         } else if (kind == G::K_INST_END) {
-          Vec3 no = base_o, nd = base_d;
-          apply_chain(P, P.insts[payload].parent, no, nd);
-          set_dir(r, no, nd);
+          inst_leave(P, P.insts[payload], r, base_o, base_d);
         } else if (kind == G::K_MEDIUM) {
           if constexpr (MEDIA) {
             /* constant_medium.rs:34-76 */
@@ -596,13 +638,12 @@ HRT_LANE Rec make_record(const KParams& P, uint32_t winner, float t, Vec3 wo, Ve
       if (pkind == G::P_RECT) {
         int k, a, b;
         plane_axes((km >> 2) & 3u, k, a, b);
-        float av = o[a] + t * d[a];
-        float bv = o[b] + t * d[b];
+        float av = comp(o, a) + t * comp(d, a);
+        float bv = comp(o, b) + t * comp(d, b);
         rec.p = o + t * d;
         rec.u = (av - p0.x) / pp->p1[1];
         rec.v = (bv - p0.z) / pp->p1[2];
-        Vec3 outward = v3(0.0f, 0.0f, 0.0f);
-        outward[k] = 1.0f;
+        const Vec3 outward = v3(k == 0 ? 1.0f : 0.0f, k == 1 ? 1.0f : 0.0f, k == 2 ? 1.0f : 0.0f);
         set_face_normal(rec, d, outward);
       } else {
         Vec3 c = v3(p0.x, p0.y, p0.z);
@@ -621,7 +662,7 @@ HRT_LANE Rec make_record(const KParams& P, uint32_t winner, float t, Vec3 wo, Ve
     /* back out through the chain, innermost first (translation.rs:32-40, rotation.rs:119-137) */
     for (uint32_t q = parent; q != G::NONE; q = P.insts[q].parent) {
       const G::Inst& in = P.insts[q];
-      if (in.kind == G::I_TRANSLATE) {
+      if ((in.kind & G::I_KIND_MASK) == G::I_TRANSLATE) {
         rec.p = rec.p + v3(in.d[0], in.d[1], in.d[2]);
         Vec3 po = wo, pd = wd; /* the ray as q's parent saw it */
         apply_chain(P, in.parent, po, pd);
@@ -629,13 +670,9 @@ HRT_LANE Rec make_record(const KParams& P, uint32_t winner, float t, Vec3 wo, Ve
       } else {
         int a = (int)(in.axis + 1) % 3, b = (int)(in.axis + 2) % 3;
         float s = in.sin_t, c = in.cos_t;
-        Vec3 p = rec.p, nn = rec.n;
-        p[a] = c * rec.p[a] - s * rec.p[b];
-        p[b] = s * rec.p[a] + c * rec.p[b];
-        nn[a] = c * rec.n[a] - s * rec.n[b];
-        nn[b] = s * rec.n[a] + c * rec.n[b];
-        rec.p = p;
-        rec.n = nn;
+        const float pa = comp(rec.p, a), pb = comp(rec.p, b), na = comp(rec.n, a), nb = comp(rec.n, b);
+        rec.p = with2(rec.p, a, c * pa - s * pb, b, s * pa + c * pb);
+        rec.n = with2(rec.n, a, c * na - s * nb, b, s * na + c * nb);
       }
     }
     return rec;
@@ -1204,13 +1241,9 @@ HRT_LANE_FI void full_step(const KParams& P, const G::Node* __restrict__ nodes,
       }
     }
   } else if (kind == G::K_INST_BEGIN) {
-    Vec3 no = r.o, nd = r.d;
-    inst_ray(P.insts[payload], no, nd);
-    set_dir(r, no, nd);
+    inst_enter(P.insts[payload], r);
   } else if (kind == G::K_INST_END) {
-    Vec3 no = wo, nd = wd;
-    apply_chain(P, P.insts[payload].parent, no, nd);
-    set_dir(r, no, nd);
+    inst_leave(P, P.insts[payload], r, wo, wd);
   } else if (kind == G::K_MEDIUM) { /* first boundary walk (constant_medium.rs:37) */
     const G::Medium& m = P.media[payload];
     w.resume = here + 1;

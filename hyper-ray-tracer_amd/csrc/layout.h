@@ -57,6 +57,11 @@ struct alignas(16) Prim {
 static_assert(sizeof(Prim) == 48, "prim is three dwordx4");
 
 enum : uint32_t { I_TRANSLATE = 0, I_ROTATE = 1 };
+/* Inst.kind = I_* | IF_* flags: what a Rotation's subtree reads of the ray beyond o and d, so that
+ * entering and leaving it recompute only that (a Translation leaves the direction, and so 1/d and
+ * d.d, unchanged): IF_INV 1/d and the inflated test's widening (box or medium nodes below),
+ * IF_DD d.d and RN(1/d.d) (spheres or media below) */
+constexpr uint32_t I_KIND_MASK = 0xFFu, IF_INV = 1u << 8, IF_DD = 1u << 9;
 struct alignas(16) Inst {
   float d[3];     /* translation displacement */
   float sin_t;    /* rotation */

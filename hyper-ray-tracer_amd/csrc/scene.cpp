@@ -344,9 +344,17 @@ struct Flattener {
         inst_depth++;
         max_inst_depth = std::max(max_inst_depth, inst_depth);
         need(inst_depth <= G::MAX_INST_DEPTH, HRT_ERR_UNSUPPORTED, "instances nested deeper than 8");
-        emit_node(G::K_INST_BEGIN, iid, nullptr);
+        const uint32_t first = emit_node(G::K_INST_BEGIN, iid, nullptr) + 1;
         emit(n.children[0], iid);
         emit_node(G::K_INST_END, iid, nullptr);
+        /* what the subtree reads of the ray beyond o, d (layout.h IF_*) */
+        for (uint32_t i = first; i + 1 < (uint32_t)s->g_nodes.size(); i++) {
+          const uint32_t kp = s->g_nodes[i].kp, k = (kp >> 24) & G::KIND_MASK;
+          if (k == G::K_BOX || k == G::K_BOX_PRIM || k == G::K_MEDIUM) s->g_insts[iid].kind |= G::IF_INV;
+          if (k == G::K_MEDIUM) s->g_insts[iid].kind |= G::IF_DD;
+          if ((k == G::K_BOX_PRIM || k == G::K_PRIM) && (s->g_prims[kp & 0xFFFFFFu].km & 3u) != G::P_RECT)
+            s->g_insts[iid].kind |= G::IF_DD;
+        }
         inst_depth--;
         return;
       }
