@@ -205,8 +205,11 @@ constexpr int general_min_waves() { return FULL && HRT_GEN_WAVES > 0 ? HRT_GEN_W
 template <bool FULL, bool LDS, bool FAST>
 constexpr int general_block_threads() { return FULL ? 256 : block_threads<LDS, FAST>(); }
 
-template <int CULL, bool FULL, bool COUNT, bool LDS, bool FAST>
-__global__ __launch_bounds__((general_block_threads<FULL, LDS, FAST>()), (general_min_waves<FULL, LDS, FAST>()))
+/* GW > 0: this instantiation is built for GW waves/SIMD (plan() picks 4 for general scenes: +18% on
+ * Cornell, +4% on Final; 3, the compiler's choice, for small noise-texture scenes, whose Perlin path
+ * spills at 128 VGPRs) */
+template <int CULL, bool FULL, bool COUNT, bool LDS, bool FAST, int GW = 0>
+__global__ __launch_bounds__((general_block_threads<FULL, LDS, FAST>()), (GW > 0 ? GW : general_min_waves<FULL, LDS, FAST>()))
 void render_kernel(KParams P) {
   extern __shared__ float4 lds_scene[];
   const G::Node* nodes = P.nodes;
@@ -671,12 +674,12 @@ int resident_grid(const void* fn, int block, int device, size_t smem, bool lds) 
   return g;
 }
 
-template <int CULL, bool FULL, bool COUNT, bool LDS, bool FAST>
+template <int CULL, bool FULL, bool COUNT, bool LDS, bool FAST, int GW = 0>
 void launch(const KParams& kp, int device, hipStream_t stream, size_t smem) {
-  const void* fn = (const void*)render_kernel<CULL, FULL, COUNT, LDS, FAST>;
+  const void* fn = (const void*)render_kernel<CULL, FULL, COUNT, LDS, FAST, GW>;
   const int block = general_block_threads<FULL, LDS, FAST>();
   const int grid = resident_grid(fn, block, device, LDS ? smem : 0, LDS);
-  hipLaunchKernelGGL((render_kernel<CULL, FULL, COUNT, LDS, FAST>), dim3(grid), dim3(block), LDS ? smem : 0, stream,
+  hipLaunchKernelGGL((render_kernel<CULL, FULL, COUNT, LDS, FAST, GW>), dim3(grid), dim3(block), LDS ? smem : 0, stream,
                      kp);
   hip_check(hipGetLastError(), "render_kernel launch");
 }
@@ -708,6 +711,7 @@ constexpr size_t LDS_GEN_MAX = 48 * 1024;
 
 struct Plan {
   bool full, fast, lds;
+  int gen_waves; /* general scenes under CULL_EXACT: the render_kernel<FULL> instantiation (3 or 4 waves/SIMD) */
   bool general; /* sphere scene forced onto the general kernel (diagnostics: HRT_KERNEL=general) */
   int cull;
   size_t smem;
@@ -740,6 +744,8 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
    * CU (HRT_GEN_LDS=0: global memory, for A/B) */
   const char* gl = getenv("HRT_GEN_LDS");
   if (pl.general && pl.full && (pl.smem > LDS_GEN_MAX || (gl && strcmp(gl, "0") == 0))) pl.lds = false;
+  const char* gw = getenv("HRT_GEN_WAVES_RT"); /* A/B override: 3 or 4 */
+  pl.gen_waves = gw ? (strcmp(gw, "3") == 0 ? 3 : 4) : ((s->feature_mask & G::F_NOISE) && pl.lds ? 3 : 4);
   return pl;
 }
 
@@ -752,8 +758,11 @@ void launch_any(const hrt_scene* s, const Plan& pl, const KParams& kp, hipStream
   } else if (pl.general) {
     const int c = pl.cull;
     if (pl.full) {
-      if (c == G::CULL_EXACT) pl.lds ? launch<G::CULL_EXACT, true, COUNT, true, false>(kp, s->device, stream, smem)
-                                     : launch<G::CULL_EXACT, true, COUNT, false, false>(kp, s->device, stream, 0);
+      if (c == G::CULL_EXACT && pl.gen_waves == 4)
+        pl.lds ? launch<G::CULL_EXACT, true, COUNT, true, false, 4>(kp, s->device, stream, smem)
+               : launch<G::CULL_EXACT, true, COUNT, false, false, 4>(kp, s->device, stream, 0);
+      else if (c == G::CULL_EXACT) pl.lds ? launch<G::CULL_EXACT, true, COUNT, true, false>(kp, s->device, stream, smem)
+                                          : launch<G::CULL_EXACT, true, COUNT, false, false>(kp, s->device, stream, 0);
       else if (c == G::CULL_SLAB) pl.lds ? launch<G::CULL_SLAB, true, COUNT, true, false>(kp, s->device, stream, smem)
                                          : launch<G::CULL_SLAB, true, COUNT, false, false>(kp, s->device, stream, 0);
       else pl.lds ? launch<G::CULL_REFERENCE, true, COUNT, true, false>(kp, s->device, stream, smem)
