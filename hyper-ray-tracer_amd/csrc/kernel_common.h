@@ -1,0 +1,188 @@
+/*
+ * kernel_common.h — what the kernel translation units share: the work claim, LDS staging, sample
+ * accumulation and counters of the persistent kernels (device), and the host helpers of the device
+ * runtime.  render.hip holds the general kernels and the runtime; render_sphere.hip the sphere-scene
+ * kernel, compiled on its own (Makefile: without the SLP vectorizer, which pairs its box-test
+ * arithmetic into v_pk_* operations that measured slower).
+ */
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "scene_internal.h"
+#include "lane.h"
+
+namespace hrt {
+
+/* host side (render.hip) */
+struct HipError {
+  hrt_status code;
+  std::string msg;
+};
+void hip_check(hipError_t e, const char* what);
+/* persistent grid: as many workgroups as are co-resident on the device (cached per kernel/device) */
+int resident_grid(const void* fn, int block, int device, size_t smem, bool lds);
+/* render_sphere.hip: launch render_basic_kernel<cull, count, lds> */
+void launch_sphere(int cull, bool count, bool lds, const lane::KParams& kp, int device, hipStream_t stream,
+                   size_t smem);
+
+namespace kern {
+namespace G = hrt::gpu;
+using namespace hrt::lane;
+
+/* COUNT builds of the sphere-scene kernel: shader-clock cycles per wave phase (s_memtime stamps,
+ * uniform per wave): [0] claim + sample start, [1] walk, [2] shading */
+struct PhaseClock {
+  unsigned long long cyc[3];
+  unsigned long long last;
+};
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+  return v;
+}
+
+/* ------------------------------------------------------------------ the megakernel */
+/* LDS: the node stream and primitive records are copied into LDS once per workgroup (they are
+ * read ~60 times per ray by dependent loads; LDS latency is a fraction of an L2 hit). */
+template <bool LDS, bool FAST>
+constexpr int block_threads() { return LDS ? (FAST ? 1024 : 512) : 256; }
+
+/* Copy the node stream and primitive records into this workgroup's LDS.  BYTE_LINKS: store each skip
+ * link as the LDS byte address of its target (base + skip x sizeof(Node)), for walks whose position is
+ * that address (basic_box STRIDE 32). */
+template <bool BYTE_LINKS = false>
+__device__ __forceinline__ void stage_scene(const KParams& P, float4* lds, const G::Node*& nodes, const G::Prim*& prims,
+                                            uint32_t base = 0u) {
+  const uint32_t n4 = P.n_nodes * (uint32_t)(sizeof(G::Node) / 16);
+  const uint32_t p4 = P.n_prims * (uint32_t)(sizeof(G::Prim) / 16);
+  const float4* gn = reinterpret_cast<const float4*>(P.nodes);
+  const float4* gp = reinterpret_cast<const float4*>(P.prims);
+  for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) {
+    float4 v = gn[k];
+    if (BYTE_LINKS && (k & 1u) == 0u) v.w = __uint_as_float(base + __float_as_uint(v.w) * (uint32_t)sizeof(G::Node));
+    lds[k] = v;
+  }
+  for (uint32_t k = threadIdx.x; k < p4; k += blockDim.x) lds[n4 + k] = gp[k];
+  __syncthreads();
+  nodes = reinterpret_cast<const G::Node*>(lds);
+  prims = reinterpret_cast<const G::Prim*>(lds + n4);
+}
+
+/* A lane's current work item: one pixel and a chunk [sample, sample_end) of its samples. */
+struct Item {
+  uint32_t pxy; /* px | py << 16 */
+  uint32_t out_idx, chunk, sample, sample_end;
+};
+
+/* Idle lanes of the wave claim work items with ONE atomicAdd (ballot + popcount).  Items are
+ * ordered [tile][8x8 block][chunk][64 pixels], so a wave starts on 64 neighbouring pixels. */
+__device__ __forceinline__ void claim_work(const KParams& P, uint32_t lane, bool& has_item, bool& exhausted,
+                                           Item& it) {
+  const bool want = !has_item && !exhausted;
+  const unsigned long long want_mask = __ballot(want);
+  if (!want_mask) return;
+  const uint32_t cnt = (uint32_t)__popcll(want_mask);
+  const int leader = __ffsll((long long)want_mask) - 1;
+  uint32_t base = 0;
+  if ((int)lane == leader) base = atomicAdd(P.counter, cnt);
+  base = __shfl(base, leader);
+  if (!want) return;
+  const uint32_t rank = (uint32_t)__popcll(want_mask & ((1ull << lane) - 1ull));
+  const uint32_t w = base + rank;
+  if (w >= P.total_work) {
+    exhausted = true;
+    return;
+  }
+  /* tile (binary search on pad_start), then [8x8 block][chunk][64 pixels] inside it */
+  uint32_t lo = 0, hi = P.n_tiles - 1;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi + 1) >> 1;
+    if (P.tiles[mid].pad_start <= w) lo = mid; else hi = mid - 1;
+  }
+  const G::TileDev T = P.tiles[lo];
+  const uint32_t q = w - T.pad_start;
+  const uint32_t blk = q / (64u * P.n_chunks), rem = q - blk * 64u * P.n_chunks;
+  const uint32_t c = rem >> 6, in = rem & 63u;
+  const uint32_t lx = (blk % T.bw) * 8u + (in & 7u), ly = (blk / T.bw) * 8u + (in >> 3);
+  if (lx < T.w && ly < T.h) {
+    has_item = true;
+    it.pxy = (T.x + lx) | ((T.y + ly) << 16);
+    it.out_idx = T.out_off + ly * T.w + lx;
+    it.chunk = c;
+    it.sample = c * P.chunk;
+    it.sample_end = min(P.spp, it.sample + P.chunk);
+  }
+}
+
+/* A finished sample: add it to the chunk sum in order (application.rs:448); a finished chunk goes to
+ * the output (one chunk: sqrt(sum/spp), alpha 1, :451-456) or to its partial-sum slot. */
+__device__ __forceinline__ void finish_sample(const KParams& P, Item& it, Vec3& sum, Vec3 rad, float scale,
+                                              bool& has_item, uint32_t& n_samples, uint32_t& n_pixels) {
+  sum = sum + rad;
+  n_samples++;
+  if (++it.sample == it.sample_end) {
+    if (P.n_chunks == 1) {
+      P.out[it.out_idx] = make_float4(sqrtf(sum.x * scale), sqrtf(sum.y * scale), sqrtf(sum.z * scale), 1.0f);
+      n_pixels++;
+    } else {
+      P.partial[(size_t)it.chunk * P.n_out + it.out_idx] = make_float4(sum.x, sum.y, sum.z, 0.0f);
+      if (it.chunk == 0) n_pixels++;
+    }
+    has_item = false;
+    sum = v3(0.0f, 0.0f, 0.0f);
+  }
+}
+
+
+__device__ __forceinline__ void flush_counts(const KParams& P, const Counts& cn) {
+  atomicAdd(&P.stats[3], (unsigned long long)cn.nodes);
+  atomicAdd(&P.stats[4], (unsigned long long)cn.prims);
+  atomicAdd(&P.stats[5], (unsigned long long)cn.tex);
+  atomicAdd(&P.stats[6], (unsigned long long)cn.walk_slots);
+  atomicAdd(&P.stats[7], (unsigned long long)cn.shade_slots);
+  atomicAdd(&P.stats[8], (unsigned long long)cn.prim_slots);
+}
+
+__device__ __forceinline__ void flush_stats(const KParams& P, uint32_t n_seg, uint32_t n_samples, uint32_t n_pixels,
+                                            const Counts& cn, bool count) {
+  atomicAdd(&P.stats[0], (unsigned long long)n_seg);
+  atomicAdd(&P.stats[1], (unsigned long long)n_samples);
+  atomicAdd(&P.stats[2], (unsigned long long)n_pixels);
+  if (count) {
+    atomicAdd(&P.stats[3], (unsigned long long)cn.nodes);
+    atomicAdd(&P.stats[4], (unsigned long long)cn.prims);
+    atomicAdd(&P.stats[5], (unsigned long long)cn.tex);
+    atomicAdd(&P.stats[6], (unsigned long long)cn.walk_slots);
+    atomicAdd(&P.stats[7], (unsigned long long)cn.shade_slots);
+    atomicAdd(&P.stats[8], (unsigned long long)cn.prim_slots);
+  }
+}
+
+#ifndef HRT_WALK_UNROLL
+#define HRT_WALK_UNROLL 6
+#endif
+constexpr int WALK_UNROLL = HRT_WALK_UNROLL; /* node steps between two checks of the wave's exit test */
+#ifndef HRT_PRIM_EVERY
+#define HRT_PRIM_EVERY HRT_WALK_UNROLL
+#endif
+constexpr int PRIM_EVERY = HRT_PRIM_EVERY; /* node steps between two checks for batched primitive tests */
+static_assert(WALK_UNROLL % PRIM_EVERY == 0, "the exit check must follow a primitive check");
+#ifndef HRT_BASIC_WAVES
+#define HRT_BASIC_WAVES 6
+#endif
+/* waves per SIMD of the sphere-scene kernel: caps its VGPRs at 512 / waves (granule 8); with the
+ * scene in LDS two workgroups share a CU, so a workgroup is 128 * waves
+ * threads (4 SIMDs x waves x 64 / 2). */
+constexpr int BASIC_WAVES = HRT_BASIC_WAVES;
+#ifndef HRT_FULL_WAVES
+#define HRT_FULL_WAVES 4
+#endif
+constexpr int FULL_WAVES = HRT_FULL_WAVES; /* waves per SIMD of render_full_kernel (it shares the workgroup shape) */
+template <bool LDS, int WAVES = BASIC_WAVES>
+constexpr int basic_block_threads() { return LDS ? 128 * WAVES : 256; }
+
+
+}  // namespace kern
+}  // namespace hrt

@@ -17,9 +17,10 @@
 #include "hrt/hrt.h"
 #include "layout.h"
 
-#define HRT_LANE __host__ __device__
+/* `inline` everywhere: lane.h is included by both kernel translation units (ODR) */
+#define HRT_LANE __host__ __device__ inline
 #define HRT_LANE_FI __host__ __device__ __forceinline__
-#define HRT_LANE_NI __host__ __device__ __attribute__((noinline))
+#define HRT_LANE_NI __host__ __device__ inline __attribute__((noinline))
 
 namespace hrt {
 namespace lane {
@@ -86,7 +87,6 @@ struct Counts {
 
 struct TRay {
   Vec3 o, d, inv;
-  Vec3 minv; /* EXACT_MARGIN * |inv|: the inflated test's widening per unit of box distance */
   float time;
   float dd;  /* dot(d, d): sphere.rs:42 `a`, constant for the ray */
   float rdd; /* RN(1 / dd) for div_rn, or NaN when dd is outside div_rn's fast domain */
@@ -131,7 +131,6 @@ HRT_LANE_FI void set_dir(TRay& r, Vec3 o, Vec3 d) {
   r.d = d;
   /* aabb.rs:22 computes 1/d per call; the value is the same every time */
   r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-  r.minv = v3(G::EXACT_MARGIN * fabsf(r.inv.x), G::EXACT_MARGIN * fabsf(r.inv.y), G::EXACT_MARGIN * fabsf(r.inv.z));
   r.dd = dot(d, d);
   r.rdd = div_rn_y(r.dd);
 }
@@ -264,67 +263,6 @@ HRT_LANE_FI bool box_ref(const float4& a, const float4& b, const TRay& r, float 
   return ok;
 }
 
-/* The inflated slab test of CULL_EXACT alone: false only if the box, widened by EXACT_MARGIN x its
- * L-inf distance D, misses the ray on [tmin, tmax].  The widening w = margin |inv_k| is folded into
- * one fma per bound (one rounding instead of two; rounding errors ~1e-7 D are far inside the 1.65x
- * slack of EXACT_MARGIN).  A NaN bound (0 * inf) is ignored by fmaxf/fminf: no constraint. */
-HRT_LANE_FI bool box_infl(const float4& a, const float4& b, const TRay& r, float tmin, float tmax) {
-#if HRT_EXP_PK && defined(__HIP_DEVICE_COMPILE__)
-  /* x and y as packed pairs (v_pk_add/mul/fma_f32: two IEEE operations per issue), z alone */
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  const f2 oxy = {r.o.x, r.o.y}, ixy = {r.inv.x, r.inv.y};
-  const f2 dmn = f2{a.x, a.y} - oxy, dmx = f2{b.x, b.y} - oxy;
-  const f2 t0 = dmn * ixy, t1 = dmx * ixy;
-  const float dmnz = a.z - r.o.z, dmxz = b.z - r.o.z;
-  const float t0z = dmnz * r.inv.z, t1z = dmxz * r.inv.z;
-  const f2 ts = {r.inv.x < 0.0f ? t1.x : t0.x, r.inv.y < 0.0f ? t1.y : t0.y};
-  const f2 te = {r.inv.x < 0.0f ? t0.x : t1.x, r.inv.y < 0.0f ? t0.y : t1.y};
-  const float tsz = r.inv.z < 0.0f ? t1z : t0z, tez = r.inv.z < 0.0f ? t0z : t1z;
-  const float dist = fmaxf(fmaxf(fmaxf(fabsf(dmn.x), fabsf(dmx.x)), fmaxf(fabsf(dmn.y), fabsf(dmx.y))),
-                           fmaxf(fabsf(dmnz), fabsf(dmxz)));
-  const float margin = G::EXACT_MARGIN * dist;
-  const f2 aixy = {fabsf(r.inv.x), fabsf(r.inv.y)};
-  const f2 lo2 = __builtin_elementwise_fma(f2{-margin, -margin}, aixy, ts);
-  const f2 hi2 = __builtin_elementwise_fma(f2{margin, margin}, aixy, te);
-  const float lo = fmaxf(fmaxf(fmaxf(tmin, lo2.x), lo2.y), fmaf(-margin, fabsf(r.inv.z), tsz));
-  const float hi = fminf(fminf(fminf(tmax, hi2.x), hi2.y), fmaf(margin, fabsf(r.inv.z), tez));
-  return !(hi < lo);
-#else
-  const float mn[3] = {a.x, a.y, a.z}, mx[3] = {b.x, b.y, b.z};
-  const float o[3] = {r.o.x, r.o.y, r.o.z}, inv[3] = {r.inv.x, r.inv.y, r.inv.z};
-  float dmn[3], dmx[3], ts[3], te[3];
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    dmn[k] = mn[k] - o[k];
-    dmx[k] = mx[k] - o[k];
-    const float t0 = dmn[k] * inv[k], t1 = dmx[k] * inv[k];
-    const bool neg = inv[k] < 0.0f;
-    ts[k] = neg ? t1 : t0;
-    te[k] = neg ? t0 : t1;
-  }
-  float dist = 0.0f;
-#pragma unroll
-  for (int k = 0; k < 3; k++) dist = fmaxf(dist, fmaxf(fabsf(dmn[k]), fabsf(dmx[k])));
-  /* widening dist * (EXACT_MARGIN |inv_k|), the per-ray factor precomputed (set_dir): it differs from
-   * (EXACT_MARGIN dist) |inv_k| by an ulp, far inside the 1.65x slack of EXACT_MARGIN.
-   * !(min(tmax, h0, h1, h2) < max(tmin, l0, l1, l2)) with NaN bounds ignored, i.e. no pair
-   * (lower, upper) out of order, written as three comparisons: the widened bounds come from fmas
-   * (canonical), so max3/min3 need no quieting, and tmin / tmax only meet comparisons (fmaxf/fminf on
-   * them cost a canonicalising v_max per operand per node step).  The fourth pair, tmin <= tmax, holds
-   * on every walk (tmax is +inf or an accepted root >= tmin). */
-  const float mi[3] = {r.minv.x, r.minv.y, r.minv.z};
-  float l[3], h[3];
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    l[k] = fmaf(-dist, mi[k], ts[k]);
-    h[k] = fmaf(dist, mi[k], te[k]);
-  }
-  const float lo = fmaxf(fmaxf(l[0], l[1]), l[2]); /* NaN only if all three are: no constraint */
-  const float hi = fminf(fminf(h[0], h[1]), h[2]);
-  return !(hi < lo) & !(hi < tmin) & !(tmax < lo);
-#endif
-}
-
 /* sphere.rs:38-55 / moving_sphere.rs:61-78 for a sphere of centre c (at the ray's time) and radius
  * `radius`: the accepted root only */
 HRT_LANE_FI bool sphere_root_at(Vec3 c, float radius, const TRay& r, float tmin, float tmax, float& root) {
@@ -430,8 +368,7 @@ HRT_LANE_FI void inst_enter(const G::Inst& in, TRay& r) {
   r.d = nd;
   if (in.kind & G::IF_INV) {
     r.inv = v3(1.0f / nd.x, 1.0f / nd.y, 1.0f / nd.z);
-    r.minv = v3(G::EXACT_MARGIN * fabsf(r.inv.x), G::EXACT_MARGIN * fabsf(r.inv.y), G::EXACT_MARGIN * fabsf(r.inv.z));
-  }
+    }
   if (in.kind & G::IF_DD) {
     r.dd = dot(nd, nd);
     r.rdd = div_rn_y(r.dd);
@@ -448,8 +385,7 @@ HRT_LANE_FI void inst_leave(const KParams& P, const G::Inst& in, TRay& r, Vec3 b
   r.d = nd;
   if (in.kind & G::IF_INV) {
     r.inv = v3(1.0f / nd.x, 1.0f / nd.y, 1.0f / nd.z);
-    r.minv = v3(G::EXACT_MARGIN * fabsf(r.inv.x), G::EXACT_MARGIN * fabsf(r.inv.y), G::EXACT_MARGIN * fabsf(r.inv.z));
-  }
+    }
   if (in.kind & G::IF_DD) {
     r.dd = dot(nd, nd);
     r.rdd = div_rn_y(r.dd);
@@ -1091,19 +1027,24 @@ HRT_LANE_FI void basic_step(const KParams& P, const G::Node* __restrict__ nodes,
  * boxes, which hold the reference boxes): false only if the box, widened by EXACT_MARGIN x D' (D' =
  * max_k |C_k - o_k| + E_k >= the L-inf distance of its farthest point from the origin), misses the ray
  * on [tmin, tmax].  Per axis the slab is m_k -+ E_k |inv_k| with m_k = (C_k - o_k) inv_k, so the
- * near/far swap of aabb.rs:28-29 disappears; the widening D' EXACT_MARGIN |inv_k| (= D' minv_k) is
- * folded into one fma.  Rounding errors of the whole computation stay below ~6 2^-24 D' |inv_k|, far
- * inside the slack of EXACT_MARGIN (layout.h: 4e-3 covers the 2.4e-3 needed 1.65 times).  A NaN bound
+ * near/far swap of aabb.rs:28-29 disappears; half-extent and widening are one product,
+ * w_k = (E_k + EXACT_MARGIN D') |inv_k| (an fma and a multiply, nothing per ray beyond 1/d).  Rounding
+ * errors of the whole computation stay below ~6 2^-24 D' |inv_k|, far inside the slack of
+ * EXACT_MARGIN (layout.h: 4e-3 covers the 2.4e-3 needed 1.65 times).  A NaN bound
  * (inv_k = +-inf: C_k = o_k or E_k = 0) is ignored by max3/min3: no constraint.  An infinite box
  * (E = +inf) always passes. */
 HRT_LANE_FI bool box_ce(const float4& a, const float4& b, const TRay& r, float tmin, float tmax) {
   const float C[3] = {a.x, a.y, a.z}, E[3] = {b.x, b.y, b.z};
   const float o[3] = {r.o.x, r.o.y, r.o.z}, inv[3] = {r.inv.x, r.inv.y, r.inv.z};
-  const float mi[3] = {r.minv.x, r.minv.y, r.minv.z};
   float m[3], e[3];
 #pragma unroll
   for (int k = 0; k < 3; k++) {
-    const float dc = C[k] - o[k];
+    float dc = C[k] - o[k];
+#if defined(__HIP_DEVICE_COMPILE__)
+    /* keep the three axes scalar: the SLP vectorizer would pair x and y into v_pk_* operations, which
+     * issue no faster than two scalar ones on gfx950 and cost moves (measured 4% slower) */
+    asm("" : "+v"(dc));
+#endif
     m[k] = dc * inv[k];
     e[k] = fabsf(dc) + E[k];
   }
@@ -1111,7 +1052,7 @@ HRT_LANE_FI bool box_ce(const float4& a, const float4& b, const TRay& r, float t
   float l[3], h[3];
 #pragma unroll
   for (int k = 0; k < 3; k++) {
-    const float w = fmaf(dist, mi[k], E[k] * fabsf(inv[k]));
+    const float w = fmaf(dist, G::EXACT_MARGIN, E[k]) * fabsf(inv[k]);
     l[k] = m[k] - w;
     h[k] = m[k] + w;
   }

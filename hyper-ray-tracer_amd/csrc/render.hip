@@ -31,28 +31,13 @@
 #include <string>
 #include <vector>
 
-#include "scene_internal.h"
+#include "kernel_common.h"
 
 using namespace hrt;
-namespace G = hrt::gpu;
-
-#include "lane.h"
-
 using namespace hrt::lane;
+using namespace hrt::kern;
 
 namespace {
-
-/* COUNT builds of the sphere-scene kernel: shader-clock cycles per wave phase (s_memtime stamps,
- * uniform per wave): [0] claim + sample start, [1] walk, [2] shading */
-struct PhaseClock {
-  unsigned long long cyc[3];
-  unsigned long long last;
-};
-
-__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
-  return v;
-}
 
 /* Diagnostics: trace ONE path (pixel, sample) and record every segment (9 floats each). */
 template <int CULL, bool FULL, bool FAST>
@@ -73,123 +58,6 @@ __global__ void debug_path_kernel(KParams P, uint32_t px, uint32_t py, uint32_t 
   out[9 * max_seg + 0] = ps.rad.x;
   out[9 * max_seg + 1] = ps.rad.y;
   out[9 * max_seg + 2] = ps.rad.z;
-}
-
-/* ------------------------------------------------------------------ the megakernel */
-/* LDS: the node stream and primitive records are copied into LDS once per workgroup (they are
- * read ~60 times per ray by dependent loads; LDS latency is a fraction of an L2 hit). */
-template <bool LDS, bool FAST>
-constexpr int block_threads() { return LDS ? (FAST ? 1024 : 512) : 256; }
-
-/* Copy the node stream and primitive records into this workgroup's LDS.  BYTE_LINKS: store each skip
- * link as the LDS byte address of its target (base + skip x sizeof(Node)), for walks whose position is
- * that address (basic_box STRIDE 32). */
-template <bool BYTE_LINKS = false>
-__device__ __forceinline__ void stage_scene(const KParams& P, float4* lds, const G::Node*& nodes, const G::Prim*& prims,
-                                            uint32_t base = 0u) {
-  const uint32_t n4 = P.n_nodes * (uint32_t)(sizeof(G::Node) / 16);
-  const uint32_t p4 = P.n_prims * (uint32_t)(sizeof(G::Prim) / 16);
-  const float4* gn = reinterpret_cast<const float4*>(P.nodes);
-  const float4* gp = reinterpret_cast<const float4*>(P.prims);
-  for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) {
-    float4 v = gn[k];
-    if (BYTE_LINKS && (k & 1u) == 0u) v.w = __uint_as_float(base + __float_as_uint(v.w) * (uint32_t)sizeof(G::Node));
-    lds[k] = v;
-  }
-  for (uint32_t k = threadIdx.x; k < p4; k += blockDim.x) lds[n4 + k] = gp[k];
-  __syncthreads();
-  nodes = reinterpret_cast<const G::Node*>(lds);
-  prims = reinterpret_cast<const G::Prim*>(lds + n4);
-}
-
-/* A lane's current work item: one pixel and a chunk [sample, sample_end) of its samples. */
-struct Item {
-  uint32_t pxy; /* px | py << 16 */
-  uint32_t out_idx, chunk, sample, sample_end;
-};
-
-/* Idle lanes of the wave claim work items with ONE atomicAdd (ballot + popcount).  Items are
- * ordered [tile][8x8 block][chunk][64 pixels], so a wave starts on 64 neighbouring pixels. */
-__device__ __forceinline__ void claim_work(const KParams& P, uint32_t lane, bool& has_item, bool& exhausted,
-                                           Item& it) {
-  const bool want = !has_item && !exhausted;
-  const unsigned long long want_mask = __ballot(want);
-  if (!want_mask) return;
-  const uint32_t cnt = (uint32_t)__popcll(want_mask);
-  const int leader = __ffsll((long long)want_mask) - 1;
-  uint32_t base = 0;
-  if ((int)lane == leader) base = atomicAdd(P.counter, cnt);
-  base = __shfl(base, leader);
-  if (!want) return;
-  const uint32_t rank = (uint32_t)__popcll(want_mask & ((1ull << lane) - 1ull));
-  const uint32_t w = base + rank;
-  if (w >= P.total_work) {
-    exhausted = true;
-    return;
-  }
-  /* tile (binary search on pad_start), then [8x8 block][chunk][64 pixels] inside it */
-  uint32_t lo = 0, hi = P.n_tiles - 1;
-  while (lo < hi) {
-    uint32_t mid = (lo + hi + 1) >> 1;
-    if (P.tiles[mid].pad_start <= w) lo = mid; else hi = mid - 1;
-  }
-  const G::TileDev T = P.tiles[lo];
-  const uint32_t q = w - T.pad_start;
-  const uint32_t blk = q / (64u * P.n_chunks), rem = q - blk * 64u * P.n_chunks;
-  const uint32_t c = rem >> 6, in = rem & 63u;
-  const uint32_t lx = (blk % T.bw) * 8u + (in & 7u), ly = (blk / T.bw) * 8u + (in >> 3);
-  if (lx < T.w && ly < T.h) {
-    has_item = true;
-    it.pxy = (T.x + lx) | ((T.y + ly) << 16);
-    it.out_idx = T.out_off + ly * T.w + lx;
-    it.chunk = c;
-    it.sample = c * P.chunk;
-    it.sample_end = min(P.spp, it.sample + P.chunk);
-  }
-}
-
-/* A finished sample: add it to the chunk sum in order (application.rs:448); a finished chunk goes to
- * the output (one chunk: sqrt(sum/spp), alpha 1, :451-456) or to its partial-sum slot. */
-__device__ __forceinline__ void finish_sample(const KParams& P, Item& it, Vec3& sum, Vec3 rad, float scale,
-                                              bool& has_item, uint32_t& n_samples, uint32_t& n_pixels) {
-  sum = sum + rad;
-  n_samples++;
-  if (++it.sample == it.sample_end) {
-    if (P.n_chunks == 1) {
-      P.out[it.out_idx] = make_float4(sqrtf(sum.x * scale), sqrtf(sum.y * scale), sqrtf(sum.z * scale), 1.0f);
-      n_pixels++;
-    } else {
-      P.partial[(size_t)it.chunk * P.n_out + it.out_idx] = make_float4(sum.x, sum.y, sum.z, 0.0f);
-      if (it.chunk == 0) n_pixels++;
-    }
-    has_item = false;
-    sum = v3(0.0f, 0.0f, 0.0f);
-  }
-}
-
-
-__device__ __forceinline__ void flush_counts(const KParams& P, const Counts& cn) {
-  atomicAdd(&P.stats[3], (unsigned long long)cn.nodes);
-  atomicAdd(&P.stats[4], (unsigned long long)cn.prims);
-  atomicAdd(&P.stats[5], (unsigned long long)cn.tex);
-  atomicAdd(&P.stats[6], (unsigned long long)cn.walk_slots);
-  atomicAdd(&P.stats[7], (unsigned long long)cn.shade_slots);
-  atomicAdd(&P.stats[8], (unsigned long long)cn.prim_slots);
-}
-
-__device__ __forceinline__ void flush_stats(const KParams& P, uint32_t n_seg, uint32_t n_samples, uint32_t n_pixels,
-                                            const Counts& cn, bool count) {
-  atomicAdd(&P.stats[0], (unsigned long long)n_seg);
-  atomicAdd(&P.stats[1], (unsigned long long)n_samples);
-  atomicAdd(&P.stats[2], (unsigned long long)n_pixels);
-  if (count) {
-    atomicAdd(&P.stats[3], (unsigned long long)cn.nodes);
-    atomicAdd(&P.stats[4], (unsigned long long)cn.prims);
-    atomicAdd(&P.stats[5], (unsigned long long)cn.tex);
-    atomicAdd(&P.stats[6], (unsigned long long)cn.walk_slots);
-    atomicAdd(&P.stats[7], (unsigned long long)cn.shade_slots);
-    atomicAdd(&P.stats[8], (unsigned long long)cn.prim_slots);
-  }
 }
 
 /* The general kernel (every feature): each iteration of the wave loop advances every busy lane by
@@ -250,194 +118,6 @@ void render_kernel(KParams P) {
     }
   }
   flush_stats(P, n_seg, n_samples, n_pixels, cn, COUNT);
-}
-
-#ifndef HRT_WALK_UNROLL
-#define HRT_WALK_UNROLL 6
-#endif
-constexpr int WALK_UNROLL = HRT_WALK_UNROLL; /* node steps between two checks of the wave's exit test */
-#ifndef HRT_PRIM_EVERY
-#define HRT_PRIM_EVERY HRT_WALK_UNROLL
-#endif
-constexpr int PRIM_EVERY = HRT_PRIM_EVERY; /* node steps between two checks for batched primitive tests */
-static_assert(WALK_UNROLL % PRIM_EVERY == 0, "the exit check must follow a primitive check");
-#ifndef HRT_BASIC_WAVES
-#define HRT_BASIC_WAVES 6
-#endif
-/* waves per SIMD of the sphere-scene kernel: caps its VGPRs at 512 / waves (granule 8); with the
- * scene in LDS two workgroups share a CU, so a workgroup is 128 * waves
- * threads (4 SIMDs x waves x 64 / 2). */
-constexpr int BASIC_WAVES = HRT_BASIC_WAVES;
-#ifndef HRT_FULL_WAVES
-#define HRT_FULL_WAVES 4
-#endif
-constexpr int FULL_WAVES = HRT_FULL_WAVES; /* waves per SIMD of render_full_kernel (it shares the workgroup shape) */
-template <bool LDS, int WAVES = BASIC_WAVES>
-constexpr int basic_block_threads() { return LDS ? 128 * WAVES : 256; }
-
-template <int CULL, bool COUNT, bool LDS>
-__global__ __launch_bounds__(basic_block_threads<LDS>(), BASIC_WAVES)
-void render_basic_kernel(KParams P) {
-  extern __shared__ float4 lds_scene[];
-  const G::Node* nodes = P.nodes;
-  const G::Prim* prims = P.prims;
-  /* CULL_EXACT walks the walk stream (layout.h; positions are byte offsets, in LDS or through a buffer
-   * descriptor); the other modes walk the reference node stream (with the scene in LDS the walk
-   * position is the node's LDS byte address, basic_box STRIDE) */
-  constexpr bool WS = CULL == G::CULL_EXACT;
-  constexpr int WMEM = LDS ? WM_LDS : WM_BUF;
-  constexpr uint32_t STRIDE = LDS ? (uint32_t)sizeof(G::Node) : 1u;
-  const uint32_t lds_base = (uint32_t)(size_t)(__attribute__((address_space(3))) float4*)lds_scene;
-  const uint32_t root = WS || !LDS ? 0u : lds_base;
-  WalkSrc ws;
-  ws.base = P.walk;
-#if defined(__HIP_DEVICE_COMPILE__)
-  ws.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)P.walk, 0, (int)P.walk_bytes, 0x00020000);
-#endif
-  if constexpr (WS && LDS) { /* the stream at LDS address 0: its offsets are LDS addresses */
-    const float4* g = reinterpret_cast<const float4*>(P.walk);
-    for (uint32_t k = threadIdx.x; k < P.walk_bytes / 16u; k += blockDim.x) lds_scene[k] = g[k];
-    __syncthreads();
-    if (lds_base != 0u) { /* no static LDS in this kernel, so this cannot happen: report, do nothing */
-      if (threadIdx.x == 0) atomicOr(&P.stats[12], 2ull);
-      return;
-    }
-  } else if constexpr (LDS) {
-    stage_scene<true>(P, lds_scene, nodes, prims, root);
-  }
-  const uint32_t lane = threadIdx.x & 63u;
-  const float scale = 1.0f / (float)P.spp; /* application.rs:403 */
-  const float inf = __uint_as_float(0x7f800000u);
-  const uint32_t end = WS ? P.walk_end : root + P.main_end * STRIDE;
-  /* t_min canonicalised once: box_ce's fmaxf against it then needs no per-step quieting */
-  const float tmin_c = __builtin_canonicalizef(P.t_min);
-  const uint32_t need = P.postpone;
-  const uint32_t batch = P.prim_batch;
-  /* watchdog: a lane's walk is at most walk_cap steps; waiting for a batch can stretch a pass to the
-   * lanes' total work (each iteration steps or tests for at least one lane) */
-  const uint32_t cap = P.walk_cap * 128u;
-
-  bool has_item = false, exhausted = false;
-  bool walking = false; /* a segment is in flight (walk running, or finished and waiting to shade) */
-  Item it{0u, 0u, 0u, 0u, 0u};
-  Vec3 sum = v3(0.0f, 0.0f, 0.0f);
-  PathState ps;
-  init_path_state(ps);
-  TRay r;
-  set_ray(r, ps.ro, ps.rd, 0.0f, P);
-  uint32_t node = G::NONE, winner = G::NONE; /* node: walk position (basic_box: index | WALK_PEND, or NONE) */
-  float closest = inf;
-  uint32_t n_seg = 0, n_samples = 0, n_pixels = 0; /* wave totals (uniform) */
-  Counts cn{0u, 0u, 0u, 0u, 0u, 0u};
-  PhaseClock pc{{0ull, 0ull, 0ull}, 0ull};
-  auto stamp = [&](int phase) {
-    if constexpr (COUNT) {
-      const unsigned long long t = __builtin_amdgcn_s_memtime();
-      if (phase >= 0) pc.cyc[phase] += t - pc.last;
-      pc.last = t;
-    }
-  };
-  stamp(-1);
-
-  for (;;) {
-    /* lanes without work claim it; lanes with work but no segment in flight start a sample */
-    claim_work(P, lane, has_item, exhausted, it);
-    if (!__any(has_item || !exhausted)) break;
-    if (has_item && !walking) {
-      start_sample(P, ps, it.pxy & 0xFFFFu, it.pxy >> 16, it.sample);
-      walking = true;
-      set_ray(r, ps.ro, ps.rd, ps.rtime, P);
-      closest = inf;
-      winner = G::NONE;
-      node = ps.depth_left == 0 ? G::NONE : root; /* max_depth 0: black without a world.hit (:478-480) */
-    }
-    /* step the walks until enough lanes have finished (lanes not walking hold node >= end).  A lane
-     * whose leaf box passed holds WALK_PEND in `node` and waits; the wave runs the sphere block
-     * once `batch` lanes wait (or no lane can step), instead of for every lane that needs it. */
-    if constexpr (COUNT) cn.shade_slots++;
-    stamp(0);
-    const unsigned long long walkers = __ballot(walking);
-    uint32_t iters = 0;
-    bool stuck = false;
-    for (;;) {
-#pragma unroll
-      for (int u = 0; u < WALK_UNROLL; u++) {
-        if constexpr (COUNT) cn.walk_slots++;
-        if (node < end) {
-          if constexpr (WS) walk_box<COUNT, WMEM>(ws, node, r, tmin_c, closest, cn);
-          else basic_box<CULL, COUNT, STRIDE>(P, nodes, node, r, closest, cn);
-        }
-        if ((u + 1) % PRIM_EVERY != 0) continue;
-        const bool waiting = walk_pending(node);
-        const unsigned long long pm = __ballot(waiting);
-        if (pm && ((uint32_t)__popcll(pm) >= batch || !__ballot(node < end))) {
-          if constexpr (COUNT) cn.prim_slots++;
-          if (waiting) {
-            if constexpr (WS) walk_prim<COUNT, WMEM>(P, ws, node, r, closest, winner, cn);
-            else basic_prim<CULL, COUNT, STRIDE>(P, nodes, prims, node, r, closest, winner, cn);
-          }
-        }
-      }
-      const unsigned long long live = __ballot(node < end || walk_pending(node));
-      if (!live || (uint32_t)__popcll(walkers & ~live) >= need) break;
-      if (++iters > cap) { stuck = true; break; }
-    }
-    if (stuck) { /* a walk that cannot end (corrupt scene data): report it, retire the wave */
-      if (lane == 0) atomicOr(&P.stats[12], 1ull);
-      exhausted = true;
-      has_item = false;
-      walking = false;
-      node = G::NONE;
-    }
-    stamp(1);
-    /* shade the finished segments (application.rs:483-494) */
-    const bool shading = walking && node >= end && !walk_pending(node);
-    const bool traced = shading && node != G::NONE;
-    bool sample_done = false, chunk_done = false;
-    if (shading) {
-      bool done = true;
-      if (traced) {
-        if constexpr (WS) done = shade_walk<COUNT, WMEM>(P, ws, ps, winner, closest, r.o, r.d, r.time, r.tau, cn);
-        else done = shade<false, COUNT>(P, ps, winner, closest, r.o, r.d, r.time, r.tau, cn);
-        done = done || ps.depth_left == 0;
-      }
-      if (done) {
-        /* application.rs:448: samples of a chunk summed in order */
-        walking = false;
-        node = G::NONE;
-        sum = sum + ps.rad;
-        sample_done = true;
-        if (++it.sample == min(P.spp, (it.chunk + 1u) * P.chunk)) {
-          if (P.n_chunks == 1) /* sqrt(sum / spp), alpha 1 (:451-456) */
-            P.out[it.out_idx] = make_float4(sqrtf(sum.x * scale), sqrtf(sum.y * scale), sqrtf(sum.z * scale), 1.0f);
-          else
-            P.partial[(size_t)it.chunk * P.n_out + it.out_idx] = make_float4(sum.x, sum.y, sum.z, 0.0f);
-          chunk_done = true;
-          has_item = false;
-          sum = v3(0.0f, 0.0f, 0.0f);
-        }
-      } else {
-        set_dir(r, ps.ro, ps.rd); /* the scattered ray keeps the sample's shutter time */
-        closest = inf;
-        winner = G::NONE;
-        node = root;
-      }
-    }
-    n_seg += (uint32_t)__popcll(__ballot(traced));
-    n_samples += (uint32_t)__popcll(__ballot(sample_done));
-    n_pixels += (uint32_t)__popcll(__ballot(chunk_done && it.chunk == 0u));
-    stamp(2);
-  }
-  if (lane == 0) {
-    atomicAdd(&P.stats[0], (unsigned long long)n_seg);
-    atomicAdd(&P.stats[1], (unsigned long long)n_samples);
-    atomicAdd(&P.stats[2], (unsigned long long)n_pixels);
-  }
-  if constexpr (COUNT) {
-    flush_counts(P, cn);
-    if (lane == 0)
-      for (int k = 0; k < 3; k++) atomicAdd(&P.stats[9 + k], pc.cyc[k]);
-  }
 }
 
 /* The general kernel with persistent walks and postponed shading (render_basic_kernel's structure;
@@ -585,15 +265,6 @@ __global__ void math_kernel(int op, const float* x, const float* y, float* out, 
 }
 
 /* ------------------------------------------------------------------ host helpers */
-struct HipError {
-  hrt_status code;
-  std::string msg;
-};
-
-void hip_check(hipError_t e, const char* what) {
-  if (e != hipSuccess) throw HipError{HRT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e)};
-}
-
 struct DeviceGuard {
   int prev = -1;
   explicit DeviceGuard(int dev) {
@@ -649,31 +320,6 @@ void take_slot_error(hrt_scene::Slot& sl) {
 }
 
 
-/* persistent grid: as many workgroups as are co-resident on the device (cached per kernel/device) */
-int resident_grid(const void* fn, int block, int device, size_t smem, bool lds) {
-  struct Key {
-    const void* fn;
-    int device;
-    size_t smem;
-    int grid;
-  };
-  static std::mutex mu;
-  static std::vector<Key> cache;
-  std::lock_guard<std::mutex> lk(mu);
-  for (const Key& k : cache)
-    if (k.fn == fn && k.device == device && k.smem == smem) return k.grid;
-  if (lds) hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem),
-                     "hipFuncSetAttribute(LDS)");
-  int per_cu = 0;
-  hip_check(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block, smem),
-            "hipOccupancyMaxActiveBlocksPerMultiprocessor");
-  hipDeviceProp_t prop;
-  hip_check(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
-  const int g = std::max(1, per_cu) * prop.multiProcessorCount;
-  cache.push_back(Key{fn, device, smem, g});
-  return g;
-}
-
 template <int CULL, bool FULL, bool COUNT, bool LDS, bool FAST, int GW = 0>
 void launch(const KParams& kp, int device, hipStream_t stream, size_t smem) {
   const void* fn = (const void*)render_kernel<CULL, FULL, COUNT, LDS, FAST, GW>;
@@ -691,15 +337,6 @@ void launch_full(const KParams& kp, int device, hipStream_t stream, size_t smem)
   const int grid = resident_grid(fn, block, device, LDS ? smem : 0, LDS);
   hipLaunchKernelGGL((render_full_kernel<CULL, COUNT, LDS>), dim3(grid), dim3(block), LDS ? smem : 0, stream, kp);
   hip_check(hipGetLastError(), "render_full_kernel launch");
-}
-
-template <int CULL, bool COUNT, bool LDS>
-void launch_basic(const KParams& kp, int device, hipStream_t stream, size_t smem) {
-  const void* fn = (const void*)render_basic_kernel<CULL, COUNT, LDS>;
-  const int block = basic_block_threads<LDS>();
-  const int grid = resident_grid(fn, block, device, LDS ? smem : 0, LDS);
-  hipLaunchKernelGGL((render_basic_kernel<CULL, COUNT, LDS>), dim3(grid), dim3(block), LDS ? smem : 0, stream, kp);
-  hip_check(hipGetLastError(), "render_basic_kernel launch");
 }
 
 /* LDS residency: the scene a sphere-kernel workgroup stages (the walk stream, or the reference-order
@@ -778,18 +415,15 @@ void launch_any(const hrt_scene* s, const Plan& pl, const KParams& kp, hipStream
   } else if (pl.cull == G::CULL_EXACT) {
     if (pl.full) pl.lds ? launch_full<G::CULL_EXACT, COUNT, true>(kp, s->device, stream, smem)
                         : launch_full<G::CULL_EXACT, COUNT, false>(kp, s->device, stream, 0);
-    else if (pl.lds) launch_basic<G::CULL_EXACT, COUNT, true>(kp, s->device, stream, smem);
-    else launch_basic<G::CULL_EXACT, COUNT, false>(kp, s->device, stream, 0);
+    else launch_sphere(G::CULL_EXACT, COUNT, pl.lds, kp, s->device, stream, smem);
   } else if (pl.cull == G::CULL_SLAB) {
     if (pl.full) pl.lds ? launch_full<G::CULL_SLAB, COUNT, true>(kp, s->device, stream, smem)
                         : launch_full<G::CULL_SLAB, COUNT, false>(kp, s->device, stream, 0);
-    else if (pl.lds) launch_basic<G::CULL_SLAB, COUNT, true>(kp, s->device, stream, smem);
-    else launch_basic<G::CULL_SLAB, COUNT, false>(kp, s->device, stream, 0);
+    else launch_sphere(G::CULL_SLAB, COUNT, pl.lds, kp, s->device, stream, smem);
   } else {
     if (pl.full) pl.lds ? launch_full<G::CULL_REFERENCE, COUNT, true>(kp, s->device, stream, smem)
                         : launch_full<G::CULL_REFERENCE, COUNT, false>(kp, s->device, stream, 0);
-    else if (pl.lds) launch_basic<G::CULL_REFERENCE, COUNT, true>(kp, s->device, stream, smem);
-    else launch_basic<G::CULL_REFERENCE, COUNT, false>(kp, s->device, stream, 0);
+    else launch_sphere(G::CULL_REFERENCE, COUNT, pl.lds, kp, s->device, stream, smem);
   }
 }
 
@@ -855,6 +489,35 @@ KParams scene_params(const hrt_scene* s, const hrt_camera* cam, const hrt_render
 
 /* ============================================================================ device runtime */
 namespace hrt {
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw HipError{HRT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e)};
+}
+
+int resident_grid(const void* fn, int block, int device, size_t smem, bool lds) {
+  struct Key {
+    const void* fn;
+    int device;
+    size_t smem;
+    int grid;
+  };
+  static std::mutex mu;
+  static std::vector<Key> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  for (const Key& k : cache)
+    if (k.fn == fn && k.device == device && k.smem == smem) return k.grid;
+  if (lds) hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem),
+                     "hipFuncSetAttribute(LDS)");
+  int per_cu = 0;
+  hip_check(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block, smem),
+            "hipOccupancyMaxActiveBlocksPerMultiprocessor");
+  hipDeviceProp_t prop;
+  hip_check(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
+  const int g = std::max(1, per_cu) * prop.multiProcessorCount;
+  cache.push_back(Key{fn, device, smem, g});
+  return g;
+}
+
 
 hrt_status device_upload(hrt_scene* s, int device) {
   return hguard([&] {

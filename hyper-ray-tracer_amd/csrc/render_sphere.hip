@@ -1,0 +1,214 @@
+/*
+ * render_sphere.hip — the sphere-scene kernel (render_basic_kernel): scenes within F_BASIC (spheres,
+ * moving spheres, Lambertian / Metal / Dielectric, solid and checker textures), among them the
+ * BASELINE headline scene.  Persistent walks over the walk stream (layout.h) with postponed shading;
+ * DESIGN.md section 6.1.  Built on its own translation unit (see kernel_common.h).
+ */
+#include "kernel_common.h"
+
+using namespace hrt;
+using namespace hrt::lane;
+using namespace hrt::kern;
+
+namespace {
+
+template <int CULL, bool COUNT, bool LDS>
+__global__ __launch_bounds__(basic_block_threads<LDS>(), BASIC_WAVES)
+void render_basic_kernel(KParams P) {
+  extern __shared__ float4 lds_scene[];
+  const G::Node* nodes = P.nodes;
+  const G::Prim* prims = P.prims;
+  /* CULL_EXACT walks the walk stream (layout.h; positions are byte offsets, in LDS or through a buffer
+   * descriptor); the other modes walk the reference node stream (with the scene in LDS the walk
+   * position is the node's LDS byte address, basic_box STRIDE) */
+  constexpr bool WS = CULL == G::CULL_EXACT;
+  constexpr int WMEM = LDS ? WM_LDS : WM_BUF;
+  constexpr uint32_t STRIDE = LDS ? (uint32_t)sizeof(G::Node) : 1u;
+  const uint32_t lds_base = (uint32_t)(size_t)(__attribute__((address_space(3))) float4*)lds_scene;
+  const uint32_t root = WS || !LDS ? 0u : lds_base;
+  WalkSrc ws;
+  ws.base = P.walk;
+#if defined(__HIP_DEVICE_COMPILE__)
+  ws.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)P.walk, 0, (int)P.walk_bytes, 0x00020000);
+#endif
+  if constexpr (WS && LDS) { /* the stream at LDS address 0: its offsets are LDS addresses */
+    const float4* g = reinterpret_cast<const float4*>(P.walk);
+    for (uint32_t k = threadIdx.x; k < P.walk_bytes / 16u; k += blockDim.x) lds_scene[k] = g[k];
+    __syncthreads();
+    if (lds_base != 0u) { /* no static LDS in this kernel, so this cannot happen: report, do nothing */
+      if (threadIdx.x == 0) atomicOr(&P.stats[12], 2ull);
+      return;
+    }
+  } else if constexpr (LDS) {
+    stage_scene<true>(P, lds_scene, nodes, prims, root);
+  }
+  const uint32_t lane = threadIdx.x & 63u;
+  const float scale = 1.0f / (float)P.spp; /* application.rs:403 */
+  const float inf = __uint_as_float(0x7f800000u);
+  const uint32_t end = WS ? P.walk_end : root + P.main_end * STRIDE;
+  /* t_min canonicalised once: box_ce's fmaxf against it then needs no per-step quieting */
+  const float tmin_c = __builtin_canonicalizef(P.t_min);
+  const uint32_t need = P.postpone;
+  const uint32_t batch = P.prim_batch;
+  /* watchdog: a lane's walk is at most walk_cap steps; waiting for a batch can stretch a pass to the
+   * lanes' total work (each iteration steps or tests for at least one lane) */
+  const uint32_t cap = P.walk_cap * 128u;
+
+  bool has_item = false, exhausted = false;
+  bool walking = false; /* a segment is in flight (walk running, or finished and waiting to shade) */
+  Item it{0u, 0u, 0u, 0u, 0u};
+  Vec3 sum = v3(0.0f, 0.0f, 0.0f);
+  PathState ps;
+  init_path_state(ps);
+  TRay r;
+  set_ray(r, ps.ro, ps.rd, 0.0f, P);
+  uint32_t node = G::NONE, winner = G::NONE; /* node: walk position (basic_box: index | WALK_PEND, or NONE) */
+  float closest = inf;
+  uint32_t n_seg = 0, n_samples = 0, n_pixels = 0; /* wave totals (uniform) */
+  Counts cn{0u, 0u, 0u, 0u, 0u, 0u};
+  PhaseClock pc{{0ull, 0ull, 0ull}, 0ull};
+  auto stamp = [&](int phase) {
+    if constexpr (COUNT) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (phase >= 0) pc.cyc[phase] += t - pc.last;
+      pc.last = t;
+    }
+  };
+  stamp(-1);
+
+  for (;;) {
+    /* lanes without work claim it; lanes with work but no segment in flight start a sample */
+    claim_work(P, lane, has_item, exhausted, it);
+    if (!__any(has_item || !exhausted)) break;
+    if (has_item && !walking) {
+      start_sample(P, ps, it.pxy & 0xFFFFu, it.pxy >> 16, it.sample);
+      walking = true;
+      set_ray(r, ps.ro, ps.rd, ps.rtime, P);
+      closest = inf;
+      winner = G::NONE;
+      node = ps.depth_left == 0 ? G::NONE : root; /* max_depth 0: black without a world.hit (:478-480) */
+    }
+    /* step the walks until enough lanes have finished (lanes not walking hold node >= end).  A lane
+     * whose leaf box passed holds WALK_PEND in `node` and waits; the wave runs the sphere block
+     * once `batch` lanes wait (or no lane can step), instead of for every lane that needs it. */
+    if constexpr (COUNT) cn.shade_slots++;
+    stamp(0);
+    const unsigned long long walkers = __ballot(walking);
+    uint32_t iters = 0;
+    bool stuck = false;
+    for (;;) {
+#pragma unroll
+      for (int u = 0; u < WALK_UNROLL; u++) {
+        if constexpr (COUNT) cn.walk_slots++;
+        if (node < end) {
+          if constexpr (WS) walk_box<COUNT, WMEM>(ws, node, r, tmin_c, closest, cn);
+          else basic_box<CULL, COUNT, STRIDE>(P, nodes, node, r, closest, cn);
+        }
+        if ((u + 1) % PRIM_EVERY != 0) continue;
+        const bool waiting = walk_pending(node);
+        const unsigned long long pm = __ballot(waiting);
+        if (pm && ((uint32_t)__popcll(pm) >= batch || !__ballot(node < end))) {
+          if constexpr (COUNT) cn.prim_slots++;
+          if (waiting) {
+            if constexpr (WS) walk_prim<COUNT, WMEM>(P, ws, node, r, closest, winner, cn);
+            else basic_prim<CULL, COUNT, STRIDE>(P, nodes, prims, node, r, closest, winner, cn);
+          }
+        }
+      }
+      const unsigned long long live = __ballot(node < end || walk_pending(node));
+      if (!live || (uint32_t)__popcll(walkers & ~live) >= need) break;
+      if (++iters > cap) { stuck = true; break; }
+    }
+    if (stuck) { /* a walk that cannot end (corrupt scene data): report it, retire the wave */
+      if (lane == 0) atomicOr(&P.stats[12], 1ull);
+      exhausted = true;
+      has_item = false;
+      walking = false;
+      node = G::NONE;
+    }
+    stamp(1);
+    /* shade the finished segments (application.rs:483-494) */
+    const bool shading = walking && node >= end && !walk_pending(node);
+    const bool traced = shading && node != G::NONE;
+    bool sample_done = false, chunk_done = false;
+    if (shading) {
+      bool done = true;
+      if (traced) {
+        if constexpr (WS) done = shade_walk<COUNT, WMEM>(P, ws, ps, winner, closest, r.o, r.d, r.time, r.tau, cn);
+        else done = shade<false, COUNT>(P, ps, winner, closest, r.o, r.d, r.time, r.tau, cn);
+        done = done || ps.depth_left == 0;
+      }
+      if (done) {
+        /* application.rs:448: samples of a chunk summed in order */
+        walking = false;
+        node = G::NONE;
+        sum = sum + ps.rad;
+        sample_done = true;
+        if (++it.sample == min(P.spp, (it.chunk + 1u) * P.chunk)) {
+          if (P.n_chunks == 1) /* sqrt(sum / spp), alpha 1 (:451-456) */
+            P.out[it.out_idx] = make_float4(sqrtf(sum.x * scale), sqrtf(sum.y * scale), sqrtf(sum.z * scale), 1.0f);
+          else
+            P.partial[(size_t)it.chunk * P.n_out + it.out_idx] = make_float4(sum.x, sum.y, sum.z, 0.0f);
+          chunk_done = true;
+          has_item = false;
+          sum = v3(0.0f, 0.0f, 0.0f);
+        }
+      } else {
+        set_dir(r, ps.ro, ps.rd); /* the scattered ray keeps the sample's shutter time */
+        closest = inf;
+        winner = G::NONE;
+        node = root;
+      }
+    }
+    n_seg += (uint32_t)__popcll(__ballot(traced));
+    n_samples += (uint32_t)__popcll(__ballot(sample_done));
+    n_pixels += (uint32_t)__popcll(__ballot(chunk_done && it.chunk == 0u));
+    stamp(2);
+  }
+  if (lane == 0) {
+    atomicAdd(&P.stats[0], (unsigned long long)n_seg);
+    atomicAdd(&P.stats[1], (unsigned long long)n_samples);
+    atomicAdd(&P.stats[2], (unsigned long long)n_pixels);
+  }
+  if constexpr (COUNT) {
+    flush_counts(P, cn);
+    if (lane == 0)
+      for (int k = 0; k < 3; k++) atomicAdd(&P.stats[9 + k], pc.cyc[k]);
+  }
+}
+
+
+template <int CULL, bool COUNT, bool LDS>
+void launch_basic(const KParams& kp, int device, hipStream_t stream, size_t smem) {
+  const void* fn = (const void*)render_basic_kernel<CULL, COUNT, LDS>;
+  const int block = basic_block_threads<LDS>();
+  const int grid = resident_grid(fn, block, device, LDS ? smem : 0, LDS);
+  hipLaunchKernelGGL((render_basic_kernel<CULL, COUNT, LDS>), dim3(grid), dim3(block), LDS ? smem : 0, stream, kp);
+  hip_check(hipGetLastError(), "render_basic_kernel launch");
+}
+
+
+}  // namespace
+
+namespace hrt {
+
+void launch_sphere(int cull, bool count, bool lds, const KParams& kp, int device, hipStream_t stream, size_t smem) {
+  if (cull == G::CULL_EXACT) {
+    if (count) lds ? launch_basic<G::CULL_EXACT, true, true>(kp, device, stream, smem)
+                   : launch_basic<G::CULL_EXACT, true, false>(kp, device, stream, 0);
+    else lds ? launch_basic<G::CULL_EXACT, false, true>(kp, device, stream, smem)
+             : launch_basic<G::CULL_EXACT, false, false>(kp, device, stream, 0);
+  } else if (cull == G::CULL_SLAB) {
+    if (count) lds ? launch_basic<G::CULL_SLAB, true, true>(kp, device, stream, smem)
+                   : launch_basic<G::CULL_SLAB, true, false>(kp, device, stream, 0);
+    else lds ? launch_basic<G::CULL_SLAB, false, true>(kp, device, stream, smem)
+             : launch_basic<G::CULL_SLAB, false, false>(kp, device, stream, 0);
+  } else {
+    if (count) lds ? launch_basic<G::CULL_REFERENCE, true, true>(kp, device, stream, smem)
+                   : launch_basic<G::CULL_REFERENCE, true, false>(kp, device, stream, 0);
+    else lds ? launch_basic<G::CULL_REFERENCE, false, true>(kp, device, stream, smem)
+             : launch_basic<G::CULL_REFERENCE, false, false>(kp, device, stream, 0);
+  }
+}
+
+}  // namespace hrt

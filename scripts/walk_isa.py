@@ -9,10 +9,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pat = sys.argv[1] if len(sys.argv) > 1 else "render_basic_kernelILi2ELb0ELb1E"
 extra = sys.argv[2:]
 out = "/tmp/walk_isa.s"
+sphere = "basic" in pat  # render_basic_kernel lives in render_sphere.hip, built without SLP (Makefile)
+src = os.path.join(ROOT, "hyper-ray-tracer_amd", "csrc", "render_sphere.hip" if sphere else "render.hip")
 subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
                 "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "hyper-ray-tracer_amd", "csrc"),
-                "--offload-arch=gfx950", "--cuda-device-only", "-S",
-                os.path.join(ROOT, "hyper-ray-tracer_amd", "csrc", "render.hip"), "-o", out] + extra,
+                "--offload-arch=gfx950", "--cuda-device-only", "-S", src, "-o", out]
+               + (["-fno-slp-vectorize"] if sphere else []) + extra,
                check=True, capture_output=True)
 s = open(out).read().split("\n")
 starts = [(i, l.split(":")[0]) for i, l in enumerate(s) if re.match(r"^_Z\S+:", l)]
