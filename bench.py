@@ -75,6 +75,8 @@ def parse():
     ap.add_argument("--no-parity", action="store_true", help="skip the oracle parity band (profiling runs)")
     ap.add_argument("--no-frame-check", action="store_true", help="N>1: skip the 1-GPU bit-identity check")
     ap.add_argument("--save", default="", help="write rank 0's last timed frame here (.pfm exact / .ppm 8-bit)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="every rank on GPU 0 (rehearsal of the N > 1 path on a one-GPU box; not a scaling figure)")
     return ap.parse_args()
 
 
@@ -233,6 +235,8 @@ def main():
         import torch.distributed as dist
 
         dist.init_process_group("gloo")  # control plane + host gather only (no RCCL, no device collective)
+    if args.one_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -380,6 +384,8 @@ def main():
         }
         if frame_check is not None:
             line["frame_check"] = frame_check
+        if args.one_device and world > 1:
+            line["note"] = "--one-device: all ranks shared GPU 0 (a rehearsal of the multi-GPU path, not a scaling figure)"
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
