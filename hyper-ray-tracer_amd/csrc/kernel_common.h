@@ -161,7 +161,7 @@ __device__ __forceinline__ void flush_stats(const KParams& P, uint32_t n_seg, ui
 }
 
 #ifndef HRT_WALK_UNROLL
-#define HRT_WALK_UNROLL 6
+#define HRT_WALK_UNROLL 8
 #endif
 constexpr int WALK_UNROLL = HRT_WALK_UNROLL; /* node steps between two checks of the wave's exit test */
 #ifndef HRT_PRIM_EVERY
