@@ -74,8 +74,9 @@ struct KParams {
   float4* partial; /* [n_chunks][n_out] chunk sums (n_chunks > 1) */
   /* sphere-scene walk stream (layout.h; render_basic_kernel under CULL_EXACT) */
   const uint8_t* walk;
-  uint32_t walk_bytes; /* whole stream (what LDS staging copies) */
+  uint32_t walk_bytes; /* whole stream */
   uint32_t walk_end;   /* byte offset one past the last record */
+  uint32_t walk_hot;   /* WM_HYB: offsets below this are staged in LDS (layout.h placement) */
 };
 
 /* per-lane work counters of the instrumented (COUNT) instantiation */
@@ -153,9 +154,10 @@ HRT_LANE_FI float4 ld4(const void* p) { return *reinterpret_cast<const float4*>(
  * byte offsets, read from LDS (the stream staged at LDS address 0), from global memory through a buffer
  * descriptor (32-bit offsets, no 64-bit address arithmetic per step), or from a host pointer (the lane
  * simulator). */
-enum : int { WM_LDS = 0, WM_BUF = 1, WM_HOST = 2 };
+enum : int { WM_LDS = 0, WM_BUF = 1, WM_HOST = 2, WM_HYB = 3 /* LDS below `hot`, global memory above */ };
 struct WalkSrc {
   const uint8_t* base; /* WM_BUF: the section in global memory; WM_HOST: the host copy */
+  uint32_t hot;        /* WM_HYB */
 #if defined(__HIP_DEVICE_COMPILE__)
   __amdgpu_buffer_rsrc_t rsrc; /* WM_BUF */
 #endif
@@ -171,6 +173,9 @@ HRT_LANE_FI float4 wload(const WalkSrc& src, uint32_t off) {
     typedef float f4v __attribute__((ext_vector_type(4)));
     const f4v v = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(src.rsrc, (int)off, 0, 0));
     return make_float4(v.x, v.y, v.z, v.w);
+  } else if constexpr (MEM == WM_HYB) {
+    if (off < src.hot) return wload<WM_LDS>(src, off);
+    return wload<WM_BUF>(src, off);
   }
 #endif
   return *reinterpret_cast<const float4*>(src.base + off);
@@ -873,12 +878,12 @@ HRT_LANE_FI bool shade_walk(const KParams& P, const WalkSrc& src, PathState& ps,
     ps.rad = ps.rad + mul_elem(ps.thr, P.background);
     return true;
   }
-  /* sphere.rs:57-73 / moving_sphere.rs:80-94 */
-  const float4 bmn = wload<MEM>(src, leaf + 32u), bmx = wload<MEM>(src, leaf + 48u);
-  const float4 s0 = wload<MEM>(src, leaf + 64u);
+  /* sphere.rs:57-73 / moving_sphere.rs:80-94 (leaf = the winning leaf's payload) */
+  const float4 bmn = wload<MEM>(src, leaf), bmx = wload<MEM>(src, leaf + 16u);
+  const float4 s0 = wload<MEM>(src, leaf + 32u);
   Vec3 c = v3(s0.x, s0.y, s0.z);
   if (f2u(bmn.w) & G::WL_MOVING) {
-    const float4 s1 = wload<MEM>(src, leaf + 80u);
+    const float4 s1 = wload<MEM>(src, leaf + 48u);
     const float f = P.motion_uniform ? tau : (rtime - s0.w) / s1.w;
     c = c + f * v3(s1.x, s1.y, s1.z);
   }
@@ -889,7 +894,7 @@ HRT_LANE_FI bool shade_walk(const KParams& P, const WalkSrc& src, PathState& ps,
   const Vec3 outward = (at - c) / bmx.w;
   rec.p = at;
   set_face_normal(rec, rd, outward);
-  const float4 ma = wload<MEM>(src, leaf + 96u), mb = wload<MEM>(src, leaf + 112u);
+  const float4 ma = wload<MEM>(src, leaf + 64u), mb = wload<MEM>(src, leaf + 80u);
   const uint32_t mw = f2u(mb.w);
   rec.mat = mw >> 8;
   const uint32_t wt = (mw >> 4) & 15u;
@@ -1078,16 +1083,16 @@ HRT_LANE_FI void walk_box(const WalkSrc& src, uint32_t& i, const TRay& r, float 
 template <bool COUNT, int MEM>
 HRT_LANE_FI void walk_prim(const KParams& P, const WalkSrc& src, uint32_t& i, const TRay& r, float& closest,
                            uint32_t& winner, Counts& cn) {
-  const uint32_t leaf = i - WALK_PEND;
-  i = leaf + G::WALK_LEAF_BYTES;
-  const float4 bmn = wload<MEM>(src, leaf + 32u), bmx = wload<MEM>(src, leaf + 48u);
+  const uint32_t leaf = i - WALK_PEND; /* the leaf's payload */
+  const float4 bmn = wload<MEM>(src, leaf), bmx = wload<MEM>(src, leaf + 16u);
   const uint32_t w = f2u(bmn.w);
+  i = w >> 2; /* the walk goes on at the leaf's pre-order successor */
   if (!(w & G::WL_NOBOX) && !box_ref(bmn, bmx, r, P.t_min, closest)) return;
   if constexpr (COUNT) cn.prims++;
-  const float4 s0 = wload<MEM>(src, leaf + 64u);
+  const float4 s0 = wload<MEM>(src, leaf + 32u);
   Vec3 c = v3(s0.x, s0.y, s0.z);
   if (w & G::WL_MOVING) { /* moving_sphere.rs:55-58 */
-    const float4 s1 = wload<MEM>(src, leaf + 80u);
+    const float4 s1 = wload<MEM>(src, leaf + 48u);
     const float f = P.motion_uniform ? r.tau : (r.time - s0.w) / s1.w;
     c = c + f * v3(s1.x, s1.y, s1.z);
   }

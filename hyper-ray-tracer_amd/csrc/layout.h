@@ -148,35 +148,39 @@ constexpr uint32_t NODE_REF_ONLY = 1u << 31;
 constexpr uint32_t KIND_MASK = 0x7Fu;
 
 /* ---------------------------------------------------------------- sphere-scene walk stream
- * What render_basic_kernel walks under CULL_EXACT: byte-addressed records in DFS pre-order, built at
- * commit from the reference stream (scene.cpp build_walk).  Same leaves in the same order as the
- * reference's BvhNode tree, so the walk tests the same primitives in the same order with the same
- * closest; the inner boxes above them may be re-grouped (any hierarchy whose
- * boxes contain their leaves' boxes gives the same result: the inflated test is conservative for any
- * box that holds the geometry, and the reference test is applied at leaves).
- *   inner (32 B): float4(C.xyz, skip)  float4(E.xyz, pass)
- *   leaf (128 B): float4(C.xyz, skip)  float4(E.xyz, pass)
- *                 float4(mn.xyz, w)    float4(mx.xyz, radius)      the reference box (aabb.rs test)
- *                 float4(c0.xyz, t0)   float4(c1 - c0, t1 - t0)    the sphere (moving_sphere.rs:55-58)
- *                 float4(A.xyz, f)     float4(B.xyz, mw)           its material, inline (shading reads no
- *                                                                  global memory): mw = M_* kind |
- *                                                                  WT_* << 4 | material index << 8;
- *                                                                  A = albedo (WT_SOLID, Metal) or the
- *                                                                  checker's odd colour, B its even
- *                                                                  colour (WT_CHECKER), f = fuzz (Metal)
- *                                                                  or ior (Dielectric); WT_GLOBAL: the
- *                                                                  texture is read from texs (any tree)
+ * What render_basic_kernel walks under CULL_EXACT: byte-addressed records built at commit from the
+ * reference stream (scene.cpp build_walk).  Same leaves in the same order as the reference's BvhNode
+ * tree, so the walk tests the same primitives in the same order with the same closest (DESIGN.md
+ * section 4); the inner boxes above them may be re-grouped (any hierarchy whose boxes contain their
+ * leaves' boxes gives the same result: the inflated test is conservative for any box that holds the
+ * geometry, and the reference test is applied at leaves).
+ *   node part (32 B), inner or leaf: float4(C.xyz, skip)  float4(E.xyz, pass)
+ *   leaf payload (96 B):  float4(mn.xyz, w)    float4(mx.xyz, radius)      the reference box (aabb.rs)
+ *                         float4(c0.xyz, t0)   float4(c1 - c0, t1 - t0)    the sphere (moving_sphere.rs:55-58)
+ *                         float4(A.xyz, f)     float4(B.xyz, mw)           its material, inline (shading reads
+ *                                                                          no global memory): mw = M_* kind |
+ *                                                                          WT_* << 4 | material index << 8;
+ *                                                                          A = albedo (WT_SOLID, Metal) or the
+ *                                                                          checker's odd colour, B its even
+ *                                                                          colour (WT_CHECKER), f = fuzz (Metal)
+ *                                                                          or ior (Dielectric); WT_GLOBAL: the
+ *                                                                          texture is read from texs (any tree)
  * C, E: centre and half-extent of a box holding the node's box ([C - E, C + E] contains [mn, mx] in
- * real arithmetic: E rounded up), for the inflated test (lane.h box_ce).  skip = byte offset one past
- * the subtree; pass = offset of the next node for an inner node, and (self | WALK_PEND) for a leaf: the
- * lane parks on the leaf until the wave runs its primitive test (walk_prim), which continues at
- * self + WALK_LEAF_BYTES.  w = WL_* flags | primitive index << 2 (the index of the prims section); the
- * walk's winner is the leaf's offset.  A leaf without a reference box (a List member: K_PRIM) has C = 0, E = +inf (the
- * inflated test always passes) and WL_NOBOX (no reference test). */
+ * real arithmetic: E rounded up), for the inflated test (lane.h box_ce).  Every link is explicit, so
+ * records may be placed anywhere: skip = the node that follows the subtree in pre-order (or the end
+ * offset); pass = the first child for an inner node, and (payload | WALK_PEND) for a leaf: the lane
+ * parks on the leaf until the wave runs its primitive test (walk_prim), which continues at the
+ * successor kept in w = WL_* flags | successor << 2.  The walk's winner is the payload's offset.  A leaf
+ * without a reference box (a List member: K_PRIM) has C = 0, E = +inf (the inflated test always
+ * passes) and WL_NOBOX (no reference test).
+ * Placement (scene.cpp walk_place_and_write): a stream within LDS_SCENE_MAX_BYTES is laid out in
+ * pre-order with each payload after its node part and staged in LDS whole; a larger one puts the node
+ * parts of the hierarchy's top levels first (breadth first, up to LDS_SCENE_MAX_BYTES: the bytes the
+ * kernel stages in LDS, w_hot), then everything else in pre-order in global memory. */
 constexpr uint32_t WALK_PEND = 1u << 31;
 /* the largest scene a sphere-kernel workgroup stages in LDS: two workgroups per CU share its 160 KiB */
 constexpr uint32_t LDS_SCENE_MAX_BYTES = 78u * 1024u;
-constexpr uint32_t WALK_INNER_BYTES = 32, WALK_LEAF_BYTES = 128;
+constexpr uint32_t WALK_NODE_BYTES = 32, WALK_PAYLOAD_BYTES = 96;
 constexpr uint32_t WL_MOVING = 1u, WL_NOBOX = 2u;
 enum : uint32_t { WT_SOLID = 0, WT_CHECKER = 1, WT_GLOBAL = 2 }; /* inline texture of a leaf's material */
 

@@ -368,8 +368,9 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
             cam->time0 >= 0.0f && cam->time1 <= 1.0f;
   pl.smem = pl.fast ? (8 * (size_t)s->f_stream_len * sizeof(G::Node) + s->f_prims.size() * sizeof(G::Prim))
                     : (s->g_nodes.size() * sizeof(G::Node) + s->g_prims.size() * sizeof(G::Prim));
-  /* the sphere kernel under CULL_EXACT stages the walk stream (layout.h) instead */
-  if (!pl.full && !pl.fast && pl.cull == G::CULL_EXACT) pl.smem = s->w_end;
+  /* the sphere kernel under CULL_EXACT stages the walk stream (layout.h) instead: whole, or its top
+   * levels (w_hot) when it exceeds the LDS budget */
+  if (!pl.full && !pl.fast && pl.cull == G::CULL_EXACT) pl.smem = s->w_hot ? s->w_hot : s->w_end;
   pl.lds = (flags & HRT_RENDER_NO_LDS) == 0 && pl.smem <= (pl.fast ? LDS_FAST_MAX : LDS_SCENE_MAX);
   const char* k = getenv("HRT_KERNEL");
   /* General scenes run the segment-at-a-time kernel by default; render_full_kernel (persistent walks)
@@ -482,6 +483,7 @@ KParams scene_params(const hrt_scene* s, const hrt_camera* cam, const hrt_render
   kp.walk = base + s->off_walk;
   kp.walk_bytes = s->w_end;
   kp.walk_end = s->w_end;
+  kp.walk_hot = pl.lds && !pl.full && !pl.fast && pl.cull == G::CULL_EXACT ? s->w_hot : 0;
   return kp;
 }
 

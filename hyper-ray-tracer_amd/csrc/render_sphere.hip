@@ -12,7 +12,9 @@ using namespace hrt::kern;
 
 namespace {
 
-template <int CULL, bool COUNT, bool LDS>
+/* HYB (CULL_EXACT with LDS): the walk stream exceeds the LDS budget; its first P.walk_hot bytes (the
+ * hierarchy's top levels) are staged, the rest is read through the buffer descriptor (layout.h) */
+template <int CULL, bool COUNT, bool LDS, bool HYB = false>
 __global__ __launch_bounds__(basic_block_threads<LDS>(), BASIC_WAVES)
 void render_basic_kernel(KParams P) {
   extern __shared__ float4 lds_scene[];
@@ -22,18 +24,20 @@ void render_basic_kernel(KParams P) {
    * descriptor); the other modes walk the reference node stream (with the scene in LDS the walk
    * position is the node's LDS byte address, basic_box STRIDE) */
   constexpr bool WS = CULL == G::CULL_EXACT;
-  constexpr int WMEM = LDS ? WM_LDS : WM_BUF;
+  constexpr int WMEM = HYB ? WM_HYB : (LDS ? WM_LDS : WM_BUF);
   constexpr uint32_t STRIDE = LDS ? (uint32_t)sizeof(G::Node) : 1u;
   const uint32_t lds_base = (uint32_t)(size_t)(__attribute__((address_space(3))) float4*)lds_scene;
   const uint32_t root = WS || !LDS ? 0u : lds_base;
   WalkSrc ws;
   ws.base = P.walk;
+  ws.hot = P.walk_hot;
 #if defined(__HIP_DEVICE_COMPILE__)
   ws.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)P.walk, 0, (int)P.walk_bytes, 0x00020000);
 #endif
   if constexpr (WS && LDS) { /* the stream at LDS address 0: its offsets are LDS addresses */
     const float4* g = reinterpret_cast<const float4*>(P.walk);
-    for (uint32_t k = threadIdx.x; k < P.walk_bytes / 16u; k += blockDim.x) lds_scene[k] = g[k];
+    const uint32_t staged = HYB ? P.walk_hot : P.walk_bytes;
+    for (uint32_t k = threadIdx.x; k < staged / 16u; k += blockDim.x) lds_scene[k] = g[k];
     __syncthreads();
     if (lds_base != 0u) { /* no static LDS in this kernel, so this cannot happen: report, do nothing */
       if (threadIdx.x == 0) atomicOr(&P.stats[12], 2ull);
@@ -178,12 +182,12 @@ void render_basic_kernel(KParams P) {
 }
 
 
-template <int CULL, bool COUNT, bool LDS>
+template <int CULL, bool COUNT, bool LDS, bool HYB = false>
 void launch_basic(const KParams& kp, int device, hipStream_t stream, size_t smem) {
-  const void* fn = (const void*)render_basic_kernel<CULL, COUNT, LDS>;
+  const void* fn = (const void*)render_basic_kernel<CULL, COUNT, LDS, HYB>;
   const int block = basic_block_threads<LDS>();
   const int grid = resident_grid(fn, block, device, LDS ? smem : 0, LDS);
-  hipLaunchKernelGGL((render_basic_kernel<CULL, COUNT, LDS>), dim3(grid), dim3(block), LDS ? smem : 0, stream, kp);
+  hipLaunchKernelGGL((render_basic_kernel<CULL, COUNT, LDS, HYB>), dim3(grid), dim3(block), LDS ? smem : 0, stream, kp);
   hip_check(hipGetLastError(), "render_basic_kernel launch");
 }
 
@@ -193,7 +197,10 @@ void launch_basic(const KParams& kp, int device, hipStream_t stream, size_t smem
 namespace hrt {
 
 void launch_sphere(int cull, bool count, bool lds, const KParams& kp, int device, hipStream_t stream, size_t smem) {
-  if (cull == G::CULL_EXACT) {
+  if (cull == G::CULL_EXACT && lds && kp.walk_hot > 0) { /* top levels in LDS, the rest in global memory */
+    if (count) launch_basic<G::CULL_EXACT, true, true, true>(kp, device, stream, smem);
+    else launch_basic<G::CULL_EXACT, false, true, true>(kp, device, stream, smem);
+  } else if (cull == G::CULL_EXACT) {
     if (count) lds ? launch_basic<G::CULL_EXACT, true, true>(kp, device, stream, smem)
                    : launch_basic<G::CULL_EXACT, true, false>(kp, device, stream, 0);
     else lds ? launch_basic<G::CULL_EXACT, false, true>(kp, device, stream, smem)

@@ -587,40 +587,138 @@ void box_ce_of(const Vec3& mn, const Vec3& mx, float* C, float* E) {
   }
 }
 
-struct WalkBuilder {
-  hrt_scene* s;
-  std::vector<float>& out;
-  uint32_t inner_bytes; /* 32, or 48 (HRT_WALK_INNER=48: a zero pad spreading records over the LDS bank
-                         * slots; measured 0.8% slower, so not the default) */
-  uint32_t words() const { return (uint32_t)out.size(); }
-  uint32_t bytes() const { return 4u * words(); }
-  static void put4(std::vector<float>& o, float a, float b, float c, float d) {
-    o.push_back(a); o.push_back(b); o.push_back(c); o.push_back(d);
+/* The hierarchy the walk stream encodes, in pre-order: a node's subtree is [i, end). */
+struct WNode {
+  Aabb box;     /* inner: the union of its leaves' boxes */
+  int32_t leaf; /* index into the leaf sequence, or -1 for an inner node */
+  uint32_t end;
+  uint32_t depth;
+};
+
+double half_area(const Aabb& b) {
+  const double x = (double)b.mx.x - b.mn.x, y = (double)b.mx.y - b.mn.y, z = (double)b.mx.z - b.mn.z;
+  return x * y + y * z + z * x;
+}
+
+Aabb box_union(const Aabb& a, const Aabb& b) {
+  Aabb u;
+  u.mn = v3(fminf(a.mn.x, b.mn.x), fminf(a.mn.y, b.mn.y), fminf(a.mn.z, b.mn.z));
+  u.mx = v3(fmaxf(a.mx.x, b.mx.x), fmaxf(a.mx.y, b.mx.y), fmaxf(a.mx.z, b.mx.z));
+  return u;
+}
+
+/* re-grouped hierarchy over leaves[0, n), iterative, pre-order (a range of n leaves is 2n - 1 nodes) */
+void walk_regroup(std::vector<WNode>& T, const std::vector<WalkLeaf>& leaves) {
+  struct Range { uint32_t lo, hi, depth; };
+  std::vector<Range> todo{{0u, (uint32_t)leaves.size(), 0u}};
+  std::vector<Aabb> pre, suf;
+  while (!todo.empty()) {
+    const Range r = todo.back();
+    todo.pop_back();
+    const uint32_t n = r.hi - r.lo, self = (uint32_t)T.size();
+    if (n == 1) {
+      T.push_back(WNode{leaves[r.lo].box, (int32_t)r.lo, self + 1, r.depth});
+      continue;
+    }
+    pre.resize(n);
+    suf.resize(n);
+    pre[0] = leaves[r.lo].box;
+    for (uint32_t k = 1; k < n; k++) pre[k] = box_union(pre[k - 1], leaves[r.lo + k].box);
+    suf[n - 1] = leaves[r.hi - 1].box;
+    for (uint32_t k = n - 1; k-- > 0;) suf[k] = box_union(suf[k + 1], leaves[r.lo + k].box);
+    /* cut after leaf k (left = [lo, lo+k], right = the rest); ties go to the cut nearest the middle */
+    uint32_t best = (n - 1) / 2;
+    double best_cost = half_area(pre[best]) * (best + 1) + half_area(suf[best + 1]) * (n - 1 - best);
+    for (uint32_t k = 0; k + 1 < n; k++) {
+      const double c = half_area(pre[k]) * (k + 1) + half_area(suf[k + 1]) * (n - 1 - k);
+      const uint32_t dk = k > (n - 1) / 2 ? k - (n - 1) / 2 : (n - 1) / 2 - k;
+      const uint32_t db = best > (n - 1) / 2 ? best - (n - 1) / 2 : (n - 1) / 2 - best;
+      if (c < best_cost || (c == best_cost && dk < db)) {
+        best_cost = c;
+        best = k;
+      }
+    }
+    T.push_back(WNode{pre[n - 1], -1, self + 2 * n - 1, r.depth});
+    todo.push_back({r.lo + best + 1, r.hi, r.depth + 1}); /* right after left */
+    todo.push_back({r.lo, r.lo + best + 1, r.depth + 1});
   }
-  void inner(const Aabb& box, uint32_t skip) {
-    float C[3], E[3];
-    box_ce_of(box.mn, box.mx, C, E);
-    const uint32_t self = bytes();
-    put4(out, C[0], C[1], C[2], u2f(skip));
-    put4(out, E[0], E[1], E[2], u2f(self + inner_bytes));
-    for (uint32_t k = G::WALK_INNER_BYTES; k < inner_bytes; k += 16) put4(out, 0.0f, 0.0f, 0.0f, 0.0f);
+}
+
+void put4(std::vector<float>& o, size_t at, float a, float b, float c, float d) {
+  o[at / 4] = a; o[at / 4 + 1] = b; o[at / 4 + 2] = c; o[at / 4 + 3] = d;
+}
+
+/* The records (layout.h): every node part at addr[i], every leaf's payload at paddr[i].  Placement:
+ * if the stream fits the LDS budget, pre-order with each payload right after its leaf (the whole
+ * stream is staged in LDS); otherwise the node parts of the hierarchy's top levels (breadth first,
+ * up to the LDS budget) come first and are staged in LDS, the rest follows in pre-order in global
+ * memory (w_hot = the staged bytes). */
+void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::vector<WalkLeaf>& leaves) {
+  const uint32_t N = (uint32_t)T.size();
+  uint64_t total = 0;
+  for (const WNode& w : T) total += G::WALK_NODE_BYTES + (w.leaf >= 0 ? G::WALK_PAYLOAD_BYTES : 0);
+  need(total < (1ull << 30), HRT_ERR_UNSUPPORTED, "scene too large for the walk stream");
+  std::vector<uint32_t> addr(N), paddr(N, 0);
+  const char* hot_env = getenv("HRT_WALK_HOT"); /* "0": no LDS-staged top levels (A/B) */
+  const bool hybrid = total > G::LDS_SCENE_MAX_BYTES && !(hot_env && strcmp(hot_env, "0") == 0);
+  uint32_t off = 0;
+  std::vector<char> hot(N, 0);
+  if (hybrid) {
+    std::vector<uint32_t> order(N);
+    for (uint32_t i = 0; i < N; i++) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return T[a].depth < T[b].depth; });
+    for (uint32_t i : order) {
+      if (off + G::WALK_NODE_BYTES > G::LDS_SCENE_MAX_BYTES) break;
+      addr[i] = off;
+      off += G::WALK_NODE_BYTES;
+      hot[i] = 1;
+    }
   }
-  void leaf(const WalkLeaf& L) {
-    const uint32_t self = bytes();
-    float C[3] = {0.0f, 0.0f, 0.0f}, E[3];
-    const float inf = u2f(0x7f800000u);
-    E[0] = E[1] = E[2] = inf;
-    if (!L.nobox) box_ce_of(L.box.mn, L.box.mx, C, E);
+  s->w_hot = hybrid ? off : 0;
+  for (uint32_t i = 0; i < N; i++) {
+    if (!hot[i]) {
+      addr[i] = off;
+      off += G::WALK_NODE_BYTES;
+    }
+    if (T[i].leaf >= 0 && !hot[i]) {
+      paddr[i] = off;
+      off += G::WALK_PAYLOAD_BYTES;
+    }
+  }
+  for (uint32_t i = 0; i < N; i++)
+    if (T[i].leaf >= 0 && hot[i]) {
+      paddr[i] = off;
+      off += G::WALK_PAYLOAD_BYTES;
+    }
+  need(off == total, HRT_ERR_STATE, "walk stream placement");
+  const uint32_t END = off;
+  if (!hybrid) s->w_hot = 0;
+  std::vector<float>& o = s->w_stream;
+  o.assign(END / 4, 0.0f);
+  const float inf = u2f(0x7f800000u);
+  for (uint32_t i = 0; i < N; i++) {
+    const WNode& w = T[i];
+    const uint32_t skip = w.end < N ? addr[w.end] : END;
+    float C[3] = {0.0f, 0.0f, 0.0f}, E[3] = {inf, inf, inf};
+    const bool nobox = w.leaf >= 0 && leaves[w.leaf].nobox;
+    if (!nobox) box_ce_of(w.box.mn, w.box.mx, C, E);
+    if (w.leaf < 0) {
+      need(i + 1 < N, HRT_ERR_STATE, "walk stream: inner node without children");
+      put4(o, addr[i], C[0], C[1], C[2], u2f(skip));
+      put4(o, addr[i] + 16, E[0], E[1], E[2], u2f(addr[i + 1])); /* pass: the first child */
+      continue;
+    }
+    const WalkLeaf& L = leaves[w.leaf];
+    put4(o, addr[i], C[0], C[1], C[2], u2f(skip));
+    put4(o, addr[i] + 16, E[0], E[1], E[2], u2f(paddr[i] | G::WALK_PEND));
     const G::Prim& p = s->g_prims[L.prim];
-    need(L.prim < (1u << 29), HRT_ERR_UNSUPPORTED, "too many primitives for the walk stream");
     const bool moving = (p.km & 3u) == G::P_MOVING;
-    const uint32_t w = (moving ? G::WL_MOVING : 0u) | (L.nobox ? G::WL_NOBOX : 0u) | (L.prim << 2);
-    put4(out, C[0], C[1], C[2], u2f(self + G::WALK_LEAF_BYTES));
-    put4(out, E[0], E[1], E[2], u2f(self | G::WALK_PEND));
-    put4(out, L.box.mn.x, L.box.mn.y, L.box.mn.z, u2f(w));
-    put4(out, L.box.mx.x, L.box.mx.y, L.box.mx.z, p.p0[3]);
-    put4(out, p.p0[0], p.p0[1], p.p0[2], moving ? p.p1[3] : 0.0f);
-    put4(out, moving ? p.p1[0] : 0.0f, moving ? p.p1[1] : 0.0f, moving ? p.p1[2] : 0.0f, moving ? p.p2[0] : 1.0f);
+    const uint32_t wflags = (moving ? G::WL_MOVING : 0u) | (L.nobox ? G::WL_NOBOX : 0u) | (skip << 2);
+    const uint32_t q = paddr[i];
+    put4(o, q, L.box.mn.x, L.box.mn.y, L.box.mn.z, u2f(wflags));
+    put4(o, q + 16, L.box.mx.x, L.box.mx.y, L.box.mx.z, p.p0[3]);
+    put4(o, q + 32, p.p0[0], p.p0[1], p.p0[2], moving ? p.p1[3] : 0.0f);
+    put4(o, q + 48, moving ? p.p1[0] : 0.0f, moving ? p.p1[1] : 0.0f, moving ? p.p1[2] : 0.0f, moving ? p.p2[0] : 1.0f);
     /* the material, inline (layout.h) */
     const uint32_t mi = p.km >> 4;
     need(mi < (1u << 24), HRT_ERR_UNSUPPORTED, "too many materials for the walk stream");
@@ -645,121 +743,55 @@ struct WalkBuilder {
         wt = G::WT_CHECKER;
       }
     }
-    put4(out, A[0], A[1], A[2], A[3]);
-    put4(out, Bc[0], Bc[1], Bc[2], u2f(m.kind | wt << 4 | mi << 8));
+    put4(o, q + 64, A[0], A[1], A[2], A[3]);
+    put4(o, q + 80, Bc[0], Bc[1], Bc[2], u2f(m.kind | wt << 4 | mi << 8));
   }
-};
-
-uint32_t walk_subtree_bytes(uint32_t n_leaves, uint32_t inner_bytes) {
-  return (n_leaves - 1) * inner_bytes + n_leaves * G::WALK_LEAF_BYTES;
-}
-
-double half_area(const Aabb& b) {
-  const double x = (double)b.mx.x - b.mn.x, y = (double)b.mx.y - b.mn.y, z = (double)b.mx.z - b.mn.z;
-  return x * y + y * z + z * x;
-}
-
-Aabb box_union(const Aabb& a, const Aabb& b) {
-  Aabb u;
-  u.mn = v3(fminf(a.mn.x, b.mn.x), fminf(a.mn.y, b.mn.y), fminf(a.mn.z, b.mn.z));
-  u.mx = v3(fmaxf(a.mx.x, b.mx.x), fmaxf(a.mx.y, b.mx.y), fmaxf(a.mx.z, b.mx.z));
-  return u;
-}
-
-/* re-grouped hierarchy over leaves[0, n): iterative, pre-order (a range's bytes are known from its
- * leaf count, so every skip link is written with its node) */
-void walk_regroup(WalkBuilder& B, const std::vector<WalkLeaf>& leaves) {
-  struct Range { uint32_t lo, hi; };
-  std::vector<Range> todo{{0u, (uint32_t)leaves.size()}};
-  std::vector<Aabb> pre, suf;
-  while (!todo.empty()) {
-    const Range r = todo.back();
-    todo.pop_back();
-    const uint32_t n = r.hi - r.lo;
-    if (n == 1) {
-      B.leaf(leaves[r.lo]);
-      continue;
-    }
-    pre.resize(n);
-    suf.resize(n);
-    pre[0] = leaves[r.lo].box;
-    for (uint32_t k = 1; k < n; k++) pre[k] = box_union(pre[k - 1], leaves[r.lo + k].box);
-    suf[n - 1] = leaves[r.hi - 1].box;
-    for (uint32_t k = n - 1; k-- > 0;) suf[k] = box_union(suf[k + 1], leaves[r.lo + k].box);
-    /* cut after leaf k (left = [lo, lo+k], right = the rest); ties go to the cut nearest the middle */
-    uint32_t best = (n - 1) / 2;
-    double best_cost = half_area(pre[best]) * (best + 1) + half_area(suf[best + 1]) * (n - 1 - best);
-    for (uint32_t k = 0; k + 1 < n; k++) {
-      const double c = half_area(pre[k]) * (k + 1) + half_area(suf[k + 1]) * (n - 1 - k);
-      const uint32_t dk = k > (n - 1) / 2 ? k - (n - 1) / 2 : (n - 1) / 2 - k;
-      const uint32_t db = best > (n - 1) / 2 ? best - (n - 1) / 2 : (n - 1) / 2 - best;
-      if (c < best_cost || (c == best_cost && dk < db)) {
-        best_cost = c;
-        best = k;
-      }
-    }
-    B.inner(pre[n - 1], B.bytes() + walk_subtree_bytes(n, B.inner_bytes));
-    todo.push_back({r.lo + best + 1, r.hi}); /* right after left */
-    todo.push_back({r.lo, r.lo + best + 1});
-  }
+  s->w_end = END;
 }
 
 void build_walk(hrt_scene* s) {
   s->w_stream.clear();
   s->w_end = 0;
+  s->w_hot = 0;
   s->w_regrouped = false;
   if ((s->feature_mask & ~G::F_BASIC) != 0) return; /* sphere scenes only */
   const uint32_t n = s->main_end;
   std::vector<WalkLeaf> leaves;
+  std::vector<WNode> T;
+  std::vector<uint32_t> open; /* reference topology: enclosing box nodes (index into T) */
   bool regroup_ok = true;
   for (uint32_t i = 0; i < n; i++) {
     const G::Node& g = s->g_nodes[i];
     const uint32_t kind = (g.kp >> 24) & G::KIND_MASK;
-    if (kind == G::K_BOX) continue;
+    while (!open.empty() && T[open.back()].end <= i) open.pop_back();
+    Aabb b;
+    b.mn = v3(g.mn[0], g.mn[1], g.mn[2]);
+    b.mx = v3(g.mx[0], g.mx[1], g.mx[2]);
+    if (kind == G::K_BOX) { /* reference topology, kept for HRT_WALK_TREE=reference and odd scenes */
+      need(g.skip > i && g.skip <= n, HRT_ERR_STATE, "walk stream: bad skip link");
+      T.push_back(WNode{b, -1, g.skip, (uint32_t)open.size()});
+      open.push_back(i);
+      continue;
+    }
     need(kind == G::K_BOX_PRIM || kind == G::K_PRIM, HRT_ERR_STATE, "walk stream: unexpected node kind");
     WalkLeaf L;
     L.nobox = kind == G::K_PRIM;
     L.prim = g.kp & 0xFFFFFFu;
-    L.box.mn = v3(g.mn[0], g.mn[1], g.mn[2]);
-    L.box.mx = v3(g.mx[0], g.mx[1], g.mx[2]);
+    L.box = b;
     if (L.nobox) regroup_ok = false;
     for (int k = 0; k < 3 && !L.nobox; k++)
       if (!(g.mn[k] <= g.mx[k]) || !std::isfinite(g.mn[k]) || !std::isfinite(g.mx[k])) regroup_ok = false;
+    T.push_back(WNode{b, (int32_t)leaves.size(), i + 1, (uint32_t)open.size()});
     leaves.push_back(L);
   }
   if (leaves.empty()) return;
   const char* mode = getenv("HRT_WALK_TREE");
-  const bool regroup = regroup_ok && !(mode && strcmp(mode, "reference") == 0);
-  const char* pad = getenv("HRT_WALK_INNER");
-  WalkBuilder B{s, s->w_stream, pad && strcmp(pad, "48") == 0 ? 48u : G::WALK_INNER_BYTES};
-  if (regroup) {
-    walk_regroup(B, leaves);
+  if (regroup_ok && !(mode && strcmp(mode, "reference") == 0)) {
+    T.clear();
+    walk_regroup(T, leaves);
     s->w_regrouped = true;
-  } else { /* the reference hierarchy, record for record */
-    std::vector<uint32_t> at(n + 1); /* node index -> byte offset */
-    uint32_t off = 0;
-    for (uint32_t i = 0; i < n; i++) {
-      at[i] = off;
-      off += ((s->g_nodes[i].kp >> 24) & G::KIND_MASK) == G::K_BOX ? B.inner_bytes : G::WALK_LEAF_BYTES;
-    }
-    at[n] = off;
-    size_t li = 0;
-    for (uint32_t i = 0; i < n; i++) {
-      const G::Node& g = s->g_nodes[i];
-      if (((g.kp >> 24) & G::KIND_MASK) == G::K_BOX) {
-        Aabb b;
-        b.mn = v3(g.mn[0], g.mn[1], g.mn[2]);
-        b.mx = v3(g.mx[0], g.mx[1], g.mx[2]);
-        need(g.skip > i && g.skip <= n, HRT_ERR_STATE, "walk stream: bad skip link");
-        B.inner(b, at[g.skip]);
-      } else {
-        B.leaf(leaves[li++]);
-      }
-    }
   }
-  s->w_end = B.bytes();
-  need(s->w_end == walk_subtree_bytes((uint32_t)leaves.size(), B.inner_bytes) || !regroup, HRT_ERR_STATE,
-       "walk stream size");
+  walk_place_and_write(s, T, leaves);
 }
 
 void flatten(hrt_scene* s) {
@@ -1247,7 +1279,8 @@ hrt_status hrt_scene_get_info(const hrt_scene* s, hrt_scene_info* info) {
     info->feature_mask = s->feature_mask;
     info->blob_bytes = (uint32_t)s->blob_bytes;
     /* the default plan (render.hip plan()): sphere scenes stage their walk stream in LDS when it fits */
-    info->in_lds = ((s->feature_mask & ~G::F_BASIC) == 0 && s->w_end > 0 && s->w_end <= G::LDS_SCENE_MAX_BYTES) ? 1u : 0u;
+    info->in_lds = ((s->feature_mask & ~G::F_BASIC) == 0 && s->w_end > 0 && s->w_end <= G::LDS_SCENE_MAX_BYTES) ? 1u
+                   : s->w_hot > 0 ? 2u : 0u;
     info->cull_mode = (uint32_t)s->cull_mode;
     info->sah_stream_len = s->f_stream_len;
     info->bvh_tied_sorts = s->bvh_tied_sorts;
@@ -1288,6 +1321,7 @@ hrt_status hrt_debug_scene_blob(hrt_scene* s, void* out, uint64_t cap, uint64_t*
       info->walk_bytes = s->w_end;
       info->walk_regrouped = s->w_regrouped ? 1u : 0u;
       info->bvh_tied_sorts = s->bvh_tied_sorts;
+      info->walk_hot = s->w_hot;
     }
   });
 }

@@ -94,6 +94,8 @@ struct hrt_scene {
   /* sphere-scene walk stream (layout.h; render_basic_kernel under CULL_EXACT): byte records */
   std::vector<float> w_stream;
   uint32_t w_end = 0;        /* bytes */
+  uint32_t w_hot = 0;        /* > 0: the stream exceeds the LDS budget; its first w_hot bytes (the top
+                              * levels' node parts) are staged in LDS, the rest is read from global memory */
   bool w_regrouped = false;  /* inner boxes re-grouped over the reference leaf order (build_walk) */
   size_t off_walk = 0;
   uint32_t feature_mask = 0;

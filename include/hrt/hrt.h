@@ -261,7 +261,7 @@ typedef struct hrt_scene_info {
   uint32_t nodes, prims, materials, textures, instances, media;
   uint32_t feature_mask;
   uint32_t blob_bytes;     /* device bytes of the flattened scene */
-  uint32_t in_lds;         /* 1 if the megakernel stages the scene in LDS */
+  uint32_t in_lds;         /* 1 if the megakernel stages the scene in LDS, 2 if only its top levels */
   uint32_t cull_mode;      /* default culling: 2 = exact (reference test + provably safe extra culling) */
   uint32_t sah_stream_len; /* >0: sphere-only scene with the SAH octant streams (8 x this many nodes) */
   /* BvhNode::new sorts of more than 20 objects with equal keys (bvh_node.rs:34): Rust's sort_unstable_by
@@ -300,6 +300,8 @@ typedef struct hrt_blob_info {
   uint32_t walk_bytes;     /* its size (0: not a sphere scene) */
   uint32_t walk_regrouped; /* its inner boxes re-grouped over the reference leaf order */
   uint32_t bvh_tied_sorts; /* as hrt_scene_info */
+  uint32_t walk_hot;       /* > 0: the walk stream's first walk_hot bytes are staged in LDS, the rest is read
+                            * from global memory (streams beyond the LDS budget) */
 } hrt_blob_info;
 hrt_status hrt_debug_scene_blob(hrt_scene* s, void* out, uint64_t cap, uint64_t* size, hrt_blob_info* info);
 /* Overwrite n bytes of the committed scene's DEVICE blob at byte `offset` (hrt_blob_info offsets), after

@@ -134,6 +134,7 @@ int lane_sim_render(const void* blob, const hrt_blob_info* bi, const hrt_camera*
   P.walk = base + bi->off_walk;
   P.walk_bytes = bi->walk_bytes;
   P.walk_end = bi->walk_bytes;
+  P.walk_hot = bi->walk_hot;
   P.cam_origin = v3(cam->origin[0], cam->origin[1], cam->origin[2]);
   P.cam_llc = v3(cam->lower_left_corner[0], cam->lower_left_corner[1], cam->lower_left_corner[2]);
   P.cam_h = v3(cam->horizontal[0], cam->horizontal[1], cam->horizontal[2]);

@@ -269,11 +269,11 @@ def test_watchdog_reports_a_killed_frame_without_stats(earth):
     ws = np.frombuffer(buf.raw, np.uint32, count=info.walk_bytes // 4, offset=info.off_walk).copy()
     off, inner = 0, 0
     while off < info.walk_bytes:
-        leaf = (ws[off // 4 + 7] & 0x80000000) != 0  # pass link with WALK_PEND: a leaf (WALK_LEAF_BYTES)
+        leaf = (ws[off // 4 + 7] & 0x80000000) != 0  # pass link with WALK_PEND: a leaf, its payload follows
         if not leaf:
             ws[off // 4 + 3] = 0
             inner += 1
-        off += 128 if leaf else 32  # layout.h WALK_LEAF_BYTES, WALK_INNER_BYTES
+        off += 128 if leaf else 32  # layout.h WALK_NODE_BYTES (+ WALK_PAYLOAD_BYTES)
     assert inner > 100
     s.poke_blob(info.off_walk, ws.tobytes())
     d = torch.zeros(W * H * 4, device="cuda")
