@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -526,6 +527,20 @@ hrt_status device_upload(hrt_scene* s, int device) {
     if (device < 0) hip_check(hipGetDevice(&device), "hipGetDevice");
     DeviceGuard dg(device);
     device_release(s);
+    /* the walk stream's re-grouped hierarchy built on the device (build_walk.hip; the host
+     * build's hierarchy node for node), for the scenes build_walk left to it (HRT_WALK_BUILD = host |
+     * device | auto: the device for scenes of at least 32768 leaves) */
+    if (s->w_regroup_pending) {
+      std::vector<host::WNode> T;
+      const std::vector<host::WalkLeaf> leaves = walk_leaves(s, nullptr, nullptr);
+      const auto t0 = std::chrono::steady_clock::now();
+      device_walk_regroup(leaves, T, device);
+      s->w_build_us = (uint32_t)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+      walk_place_and_write(s, T, leaves);
+      s->w_device_built = true;
+      s->w_regrouped = true;
+      s->w_regroup_pending = false;
+    }
     std::vector<uint8_t> blob = build_blob(s);
     const size_t off = blob.size();
     s->device = device; /* from here on device_release() cleans up whatever was allocated */

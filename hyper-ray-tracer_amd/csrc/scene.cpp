@@ -12,6 +12,7 @@
  *   counts           hittable/.rs count() (Rotation::count == 1, rotation.rs:140-142)
  */
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -567,12 +568,6 @@ void build_fast(hrt_scene* s) {
  * leaves' boxes gives the reference's result.  The reference hierarchy itself is
  * kept (HRT_WALK_TREE=reference) for A/B, and whenever a leaf has no box or a box that is not a finite
  * well-formed interval. */
-struct WalkLeaf {
-  Aabb box;
-  bool nobox;
-  uint32_t prim;
-};
-
 /* centre / half-extent of a box, E rounded up so that [C - E, C + E] holds [mn, mx] exactly */
 void box_ce_of(const Vec3& mn, const Vec3& mx, float* C, float* E) {
   for (int k = 0; k < 3; k++) {
@@ -586,14 +581,6 @@ void box_ce_of(const Vec3& mn, const Vec3& mx, float* C, float* E) {
     E[k] = ef;
   }
 }
-
-/* The hierarchy the walk stream encodes, in pre-order: a node's subtree is [i, end). */
-struct WNode {
-  Aabb box;     /* inner: the union of its leaves' boxes */
-  int32_t leaf; /* index into the leaf sequence, or -1 for an inner node */
-  uint32_t end;
-  uint32_t depth;
-};
 
 double half_area(const Aabb& b) {
   const double x = (double)b.mx.x - b.mn.x, y = (double)b.mx.y - b.mn.y, z = (double)b.mx.z - b.mn.z;
@@ -648,6 +635,92 @@ void put4(std::vector<float>& o, size_t at, float a, float b, float c, float d) 
   o[at / 4] = a; o[at / 4 + 1] = b; o[at / 4 + 2] = c; o[at / 4 + 3] = d;
 }
 
+}  // namespace
+namespace hrt {
+void build_walk(hrt_scene* s);
+}
+namespace {
+using hrt::build_walk;
+
+void flatten(hrt_scene* s) {
+  s->g_nodes.clear(); s->g_prims.clear(); s->g_insts.clear(); s->g_media.clear();
+  s->g_mats.clear(); s->g_texs.clear();
+  s->feature_mask = 0;
+  s->all_boxes_ok = true;
+  /* materials and textures first (media append their isotropic materials after these) */
+  for (const HMat& m : s->mats) {
+    G::Mat g;
+    memset(&g, 0, sizeof(g));
+    g.kind = m.kind;
+    g.tex = m.tex == G::NONE ? 0 : m.tex;
+    if (m.kind == G::M_METAL) {
+      g.a[0] = m.albedo.x; g.a[1] = m.albedo.y; g.a[2] = m.albedo.z; g.a[3] = m.fuzz;
+      s->feature_mask |= G::F_METAL;
+    } else if (m.kind == G::M_DIELECTRIC) {
+      g.a[0] = m.ior;
+      s->feature_mask |= G::F_DIELECTRIC;
+    } else {
+      g.needs_uv = tex_needs_uv(s, m.tex) ? 1u : 0u;
+      s->feature_mask |= tex_features(s, m.tex);
+      if (m.kind == G::M_DIFFUSE_LIGHT) s->feature_mask |= G::F_LIGHT;
+      if (m.kind == G::M_ISOTROPIC) s->feature_mask |= G::F_ISOTROPIC;
+    }
+    s->g_mats.push_back(g);
+  }
+  for (const HTex& t : s->texs) {
+    G::Tex g;
+    memset(&g, 0, sizeof(g));
+    g.kind = t.kind;
+    if (t.kind == G::T_SOLID) { g.a[0] = t.color.x; g.a[1] = t.color.y; g.a[2] = t.color.z; }
+    else if (t.kind == G::T_CHECKER) { g.i0 = t.odd; g.i1 = t.even; }
+    else if (t.kind == G::T_NOISE) { g.a[0] = t.scale; g.i0 = t.perlin; }
+    else { g.i0 = (uint32_t)t.img_off; g.i1 = t.w; g.i2 = t.h; g.i3 = t.c; }
+    s->g_texs.push_back(g);
+  }
+  Flattener f{s, {}, false, 0, 0};
+  f.emit(s->root, G::NONE);
+  s->main_end = (uint32_t)s->g_nodes.size();
+  f.in_boundary = true;
+  for (size_t i = 0; i < f.pending.size(); i++) {
+    uint32_t bstart = (uint32_t)s->g_nodes.size();
+    f.emit(f.pending[i].boundary, G::NONE);
+    s->g_media[f.pending[i].medium].bstart = bstart;
+    s->g_media[f.pending[i].medium].bend = (uint32_t)s->g_nodes.size();
+  }
+  for (const G::Medium& m : s->g_media) s->feature_mask |= tex_features(s, s->g_mats[m.mat].tex);
+  /* Default culling: the reference's per-axis test AND the provably safe inflated slab test
+   * (layout.h CULL_EXACT; boxes that may not hold their geometry are flagged NODE_REF_ONLY). */
+  bool sphere_only = (s->feature_mask & (G::F_RECT | G::F_INSTANCE | G::F_MEDIUM)) == 0;
+  s->cull_mode = G::CULL_EXACT;
+  s->ln_e = ln_f(E_F);
+  /* moving_sphere.rs:55-58 divides by (time1 - time0) per call; when every moving sphere has the
+   * same time0 and time1 (all reference scenes) the quotient depends on the ray only */
+  s->motion_uniform = true;
+  bool first = true;
+  for (const G::Prim& p : s->g_prims) {
+    if ((p.km & 3u) != G::P_MOVING) continue;
+    if (first) {
+      s->motion_t0 = p.p1[3];
+      s->motion_span = p.p2[0];
+      first = false;
+    } else if (memcmp(&s->motion_t0, &p.p1[3], 4) != 0 || memcmp(&s->motion_span, &p.p2[0], 4) != 0) {
+      s->motion_uniform = false;
+    }
+  }
+  if (first) s->motion_uniform = false; /* no moving sphere */
+  s->media_nested = false;
+  for (const G::Medium& m : s->g_media) s->media_nested |= m.parent != G::NONE;
+  s->f_nodes.clear();
+  s->f_prims.clear();
+  s->f_stream_len = 0;
+  if (sphere_only && (s->feature_mask & ~G::F_BASIC) == 0) build_fast(s); /* opt-in approximate path */
+  build_walk(s);
+}
+
+}  // namespace
+
+
+namespace hrt {
 /* The records (layout.h): every node part at addr[i], every leaf's payload at paddr[i].  Placement:
  * if the stream fits the LDS budget, pre-order with each payload right after its leaf (the whole
  * stream is staged in LDS); otherwise the node parts of the hierarchy's top levels (breadth first,
@@ -749,17 +822,13 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
   s->w_end = END;
 }
 
-void build_walk(hrt_scene* s) {
-  s->w_stream.clear();
-  s->w_end = 0;
-  s->w_hot = 0;
-  s->w_regrouped = false;
-  if ((s->feature_mask & ~G::F_BASIC) != 0) return; /* sphere scenes only */
+/* The leaf sequence of the reference stream (its pre-order) and the reference hierarchy over it. */
+std::vector<WalkLeaf> walk_leaves(const hrt_scene* s, std::vector<WNode>* ref_tree, bool* regroup_ok) {
   const uint32_t n = s->main_end;
   std::vector<WalkLeaf> leaves;
+  std::vector<uint32_t> open; /* enclosing box nodes (index into the reference tree) */
   std::vector<WNode> T;
-  std::vector<uint32_t> open; /* reference topology: enclosing box nodes (index into T) */
-  bool regroup_ok = true;
+  bool ok = true;
   for (uint32_t i = 0; i < n; i++) {
     const G::Node& g = s->g_nodes[i];
     const uint32_t kind = (g.kp >> 24) & G::KIND_MASK;
@@ -767,7 +836,7 @@ void build_walk(hrt_scene* s) {
     Aabb b;
     b.mn = v3(g.mn[0], g.mn[1], g.mn[2]);
     b.mx = v3(g.mx[0], g.mx[1], g.mx[2]);
-    if (kind == G::K_BOX) { /* reference topology, kept for HRT_WALK_TREE=reference and odd scenes */
+    if (kind == G::K_BOX) {
       need(g.skip > i && g.skip <= n, HRT_ERR_STATE, "walk stream: bad skip link");
       T.push_back(WNode{b, -1, g.skip, (uint32_t)open.size()});
       open.push_back(i);
@@ -778,99 +847,46 @@ void build_walk(hrt_scene* s) {
     L.nobox = kind == G::K_PRIM;
     L.prim = g.kp & 0xFFFFFFu;
     L.box = b;
-    if (L.nobox) regroup_ok = false;
+    if (L.nobox) ok = false;
     for (int k = 0; k < 3 && !L.nobox; k++)
-      if (!(g.mn[k] <= g.mx[k]) || !std::isfinite(g.mn[k]) || !std::isfinite(g.mx[k])) regroup_ok = false;
+      if (!(g.mn[k] <= g.mx[k]) || !std::isfinite(g.mn[k]) || !std::isfinite(g.mx[k])) ok = false;
     T.push_back(WNode{b, (int32_t)leaves.size(), i + 1, (uint32_t)open.size()});
     leaves.push_back(L);
   }
+  if (ref_tree) *ref_tree = std::move(T);
+  if (regroup_ok) *regroup_ok = ok;
+  return leaves;
+}
+
+void build_walk(hrt_scene* s) {
+  s->w_stream.clear();
+  s->w_end = 0;
+  s->w_hot = 0;
+  s->w_regrouped = false;
+  s->w_device_built = false;
+  s->w_regroup_pending = false;
+  if ((s->feature_mask & ~G::F_BASIC) != 0) return; /* sphere scenes only */
+  std::vector<WNode> T;
+  bool regroup_ok = false;
+  const std::vector<WalkLeaf> leaves = walk_leaves(s, &T, &regroup_ok);
   if (leaves.empty()) return;
   const char* mode = getenv("HRT_WALK_TREE");
-  if (regroup_ok && !(mode && strcmp(mode, "reference") == 0)) {
+  const char* wb = getenv("HRT_WALK_BUILD"); /* host | device | auto (default) */
+  const bool regroup = regroup_ok && !(mode && strcmp(mode, "reference") == 0);
+  /* large scenes are re-grouped on the device at upload (build_walk.hip): until then the
+   * stream keeps the reference hierarchy (valid for the host-side tools that read it) */
+  if (regroup && (wb ? strcmp(wb, "device") == 0 : leaves.size() >= 32768)) s->w_regroup_pending = true;
+  else if (regroup) {
+    const auto t0 = std::chrono::steady_clock::now();
     T.clear();
     walk_regroup(T, leaves);
+    s->w_build_us = (uint32_t)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
     s->w_regrouped = true;
   }
   walk_place_and_write(s, T, leaves);
 }
 
-void flatten(hrt_scene* s) {
-  s->g_nodes.clear(); s->g_prims.clear(); s->g_insts.clear(); s->g_media.clear();
-  s->g_mats.clear(); s->g_texs.clear();
-  s->feature_mask = 0;
-  s->all_boxes_ok = true;
-  /* materials and textures first (media append their isotropic materials after these) */
-  for (const HMat& m : s->mats) {
-    G::Mat g;
-    memset(&g, 0, sizeof(g));
-    g.kind = m.kind;
-    g.tex = m.tex == G::NONE ? 0 : m.tex;
-    if (m.kind == G::M_METAL) {
-      g.a[0] = m.albedo.x; g.a[1] = m.albedo.y; g.a[2] = m.albedo.z; g.a[3] = m.fuzz;
-      s->feature_mask |= G::F_METAL;
-    } else if (m.kind == G::M_DIELECTRIC) {
-      g.a[0] = m.ior;
-      s->feature_mask |= G::F_DIELECTRIC;
-    } else {
-      g.needs_uv = tex_needs_uv(s, m.tex) ? 1u : 0u;
-      s->feature_mask |= tex_features(s, m.tex);
-      if (m.kind == G::M_DIFFUSE_LIGHT) s->feature_mask |= G::F_LIGHT;
-      if (m.kind == G::M_ISOTROPIC) s->feature_mask |= G::F_ISOTROPIC;
-    }
-    s->g_mats.push_back(g);
-  }
-  for (const HTex& t : s->texs) {
-    G::Tex g;
-    memset(&g, 0, sizeof(g));
-    g.kind = t.kind;
-    if (t.kind == G::T_SOLID) { g.a[0] = t.color.x; g.a[1] = t.color.y; g.a[2] = t.color.z; }
-    else if (t.kind == G::T_CHECKER) { g.i0 = t.odd; g.i1 = t.even; }
-    else if (t.kind == G::T_NOISE) { g.a[0] = t.scale; g.i0 = t.perlin; }
-    else { g.i0 = (uint32_t)t.img_off; g.i1 = t.w; g.i2 = t.h; g.i3 = t.c; }
-    s->g_texs.push_back(g);
-  }
-  Flattener f{s, {}, false, 0, 0};
-  f.emit(s->root, G::NONE);
-  s->main_end = (uint32_t)s->g_nodes.size();
-  f.in_boundary = true;
-  for (size_t i = 0; i < f.pending.size(); i++) {
-    uint32_t bstart = (uint32_t)s->g_nodes.size();
-    f.emit(f.pending[i].boundary, G::NONE);
-    s->g_media[f.pending[i].medium].bstart = bstart;
-    s->g_media[f.pending[i].medium].bend = (uint32_t)s->g_nodes.size();
-  }
-  for (const G::Medium& m : s->g_media) s->feature_mask |= tex_features(s, s->g_mats[m.mat].tex);
-  /* Default culling: the reference's per-axis test AND the provably safe inflated slab test
-   * (layout.h CULL_EXACT; boxes that may not hold their geometry are flagged NODE_REF_ONLY). */
-  bool sphere_only = (s->feature_mask & (G::F_RECT | G::F_INSTANCE | G::F_MEDIUM)) == 0;
-  s->cull_mode = G::CULL_EXACT;
-  s->ln_e = ln_f(E_F);
-  /* moving_sphere.rs:55-58 divides by (time1 - time0) per call; when every moving sphere has the
-   * same time0 and time1 (all reference scenes) the quotient depends on the ray only */
-  s->motion_uniform = true;
-  bool first = true;
-  for (const G::Prim& p : s->g_prims) {
-    if ((p.km & 3u) != G::P_MOVING) continue;
-    if (first) {
-      s->motion_t0 = p.p1[3];
-      s->motion_span = p.p2[0];
-      first = false;
-    } else if (memcmp(&s->motion_t0, &p.p1[3], 4) != 0 || memcmp(&s->motion_span, &p.p2[0], 4) != 0) {
-      s->motion_uniform = false;
-    }
-  }
-  if (first) s->motion_uniform = false; /* no moving sphere */
-  s->media_nested = false;
-  for (const G::Medium& m : s->g_media) s->media_nested |= m.parent != G::NONE;
-  s->f_nodes.clear();
-  s->f_prims.clear();
-  s->f_stream_len = 0;
-  if (sphere_only && (s->feature_mask & ~G::F_BASIC) == 0) build_fast(s); /* opt-in approximate path */
-  build_walk(s);
-}
-
-}  // namespace
-
+}  // namespace hrt
 namespace hrt {
 void flatten_scene(hrt_scene* s) { flatten(s); }
 
@@ -1285,6 +1301,8 @@ hrt_status hrt_scene_get_info(const hrt_scene* s, hrt_scene_info* info) {
     info->sah_stream_len = s->f_stream_len;
     info->bvh_tied_sorts = s->bvh_tied_sorts;
     info->walk_regrouped = s->w_regrouped ? 1u : 0u;
+    info->walk_device_built = s->w_device_built ? 1u : 0u;
+    info->walk_build_us = s->w_build_us;
   });
 }
 

@@ -62,6 +62,20 @@ struct HMat {
   float fuzz = 0, ior = 0;
 };
 
+/* the sphere kernel's walk stream (layout.h): a leaf of the reference stream, and the hierarchy the
+ * stream encodes, in pre-order (a node's subtree is [i, end)) */
+struct WalkLeaf {
+  Aabb box;
+  bool nobox;
+  uint32_t prim;
+};
+struct WNode {
+  Aabb box;     /* inner: the union of its leaves' boxes */
+  int32_t leaf; /* index into the leaf sequence, or -1 for an inner node */
+  uint32_t end;
+  uint32_t depth;
+};
+
 }  // namespace host
 }  // namespace hrt
 
@@ -97,6 +111,9 @@ struct hrt_scene {
   uint32_t w_hot = 0;        /* > 0: the stream exceeds the LDS budget; its first w_hot bytes (the top
                               * levels' node parts) are staged in LDS, the rest is read from global memory */
   bool w_regrouped = false;  /* inner boxes re-grouped over the reference leaf order (build_walk) */
+  bool w_device_built = false; /* ... by the device-side build (build_walk.hip) */
+  bool w_regroup_pending = false; /* re-grouping left to the device build at upload */
+  uint32_t w_build_us = 0;   /* time of the re-grouping (host or device) */
   size_t off_walk = 0;
   uint32_t feature_mask = 0;
   int cull_mode = hrt::gpu::CULL_REFERENCE;
@@ -138,5 +155,11 @@ void set_error(const std::string& msg);
 hrt_status device_upload(hrt_scene* s, int device);
 void flatten_scene(hrt_scene* s);          /* scene.cpp: graph -> layout.h arrays */
 std::vector<uint8_t> build_blob(hrt_scene* s); /* scene.cpp: the arrays in one blob; sets s->off_* */
+/* scene.cpp: the walk stream's leaves (with the reference hierarchy and whether it may be re-grouped),
+ * and the placement + records of a hierarchy over them */
+std::vector<host::WalkLeaf> walk_leaves(const hrt_scene* s, std::vector<host::WNode>* ref_tree, bool* regroup_ok);
+void walk_place_and_write(hrt_scene* s, const std::vector<host::WNode>& T, const std::vector<host::WalkLeaf>& leaves);
+/* build_walk.hip: the re-grouped hierarchy (scene.cpp walk_regroup's splits) built on the device */
+void device_walk_regroup(const std::vector<host::WalkLeaf>& leaves, std::vector<host::WNode>& T, int device);
 void device_release(hrt_scene* s);
 }  // namespace hrt

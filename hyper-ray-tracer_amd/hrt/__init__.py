@@ -125,7 +125,7 @@ class SceneInfo(ctypes.Structure):
     _fields_ = [
         (n, ctypes.c_uint32)
         for n in ("nodes", "prims", "materials", "textures", "instances", "media", "feature_mask", "blob_bytes", "in_lds",
-                  "cull_mode", "sah_stream_len", "bvh_tied_sorts", "walk_regrouped")
+                  "cull_mode", "sah_stream_len", "bvh_tied_sorts", "walk_regrouped", "walk_device_built", "walk_build_us")
     ]
 
 

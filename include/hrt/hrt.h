@@ -269,6 +269,8 @@ typedef struct hrt_scene_info {
    * insertion sort), so 0 means the BVH topology is the reference's for any Rust version */
   uint32_t bvh_tied_sorts;
   uint32_t walk_regrouped; /* sphere scenes: the walk stream's inner boxes are re-grouped (layout.h) */
+  uint32_t walk_device_built; /* ... by the device-side build (HRT_WALK_BUILD) */
+  uint32_t walk_build_us;  /* the re-grouping's time, host or device (us) */
 } hrt_scene_info;
 hrt_status hrt_scene_get_info(const hrt_scene* s, hrt_scene_info* info);
 /* Write an RGBA f32 frame (w x h, row-major, row 0 = image y 0 = bottom, as the render calls produce;
