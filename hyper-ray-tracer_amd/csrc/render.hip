@@ -491,6 +491,43 @@ KParams scene_params(const hrt_scene* s, const hrt_camera* cam, const hrt_render
 }  // namespace
 
 /* ============================================================================ device runtime */
+namespace {
+/* hrt_render's device output buffers (scene_internal.h out_pool): taken and given back under the pool's
+ * mutex; a buffer too small for a call is freed and replaced */
+struct OutBuf {
+  void* ptr;
+  size_t cap;
+};
+struct OutPool {
+  std::mutex mu;
+  std::vector<OutBuf> free;
+};
+OutBuf out_pool_take(hrt_scene* s, size_t bytes) {
+  OutPool* pool = static_cast<OutPool*>(s->out_pool);
+  OutBuf b{nullptr, 0};
+  {
+    std::lock_guard<std::mutex> lk(pool->mu);
+    if (!pool->free.empty()) {
+      b = pool->free.back();
+      pool->free.pop_back();
+    }
+  }
+  if (b.cap < bytes) {
+    if (b.ptr) hip_check(hipFree(b.ptr), "hipFree(out)");
+    b = OutBuf{nullptr, 0};
+    hip_check(hipMalloc(&b.ptr, bytes), "hipMalloc(out)");
+    b.cap = bytes;
+  }
+  return b;
+}
+void out_pool_give(hrt_scene* s, OutBuf b) {
+  if (!b.ptr) return;
+  OutPool* pool = static_cast<OutPool*>(s->out_pool);
+  std::lock_guard<std::mutex> lk(pool->mu);
+  pool->free.push_back(b);
+}
+}  // namespace
+
 namespace hrt {
 
 void hip_check(hipError_t e, const char* what) {
@@ -547,6 +584,7 @@ hrt_status device_upload(hrt_scene* s, int device) {
     hip_check(hipMalloc(&s->d_blob, off), "hipMalloc(scene)");
     hip_check(hipMemcpy(s->d_blob, blob.data(), off, hipMemcpyHostToDevice), "hipMemcpy(scene)");
     s->slot_mutex = new std::mutex();
+    s->out_pool = new OutPool();
     for (auto& sl : s->slots) {
       hipEvent_t ev;
       hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
@@ -574,6 +612,11 @@ void device_release(hrt_scene* s) {
   }
   delete static_cast<std::mutex*>(s->slot_mutex);
   s->slot_mutex = nullptr;
+  if (OutPool* pool = static_cast<OutPool*>(s->out_pool)) {
+    for (const OutBuf& b : pool->free) (void)hipFree(b.ptr);
+    delete pool;
+  }
+  s->out_pool = nullptr;
   if (s->d_blob) (void)hipFree(s->d_blob);
   s->d_blob = nullptr;
   if (prev >= 0) (void)hipSetDevice(prev);
@@ -734,27 +777,24 @@ hrt_status hrt_render(hrt_scene* s, const hrt_camera* cam, const hrt_render_para
     set_error("hrt_render: null argument or scene not committed");
     return (s && !s->committed) ? HRT_ERR_STATE : HRT_ERR_INVALID_ARG;
   }
-  float* d_out = nullptr;
+  /* the device output buffer comes from the scene's pool (allocated once, reused by every later call,
+   * e.g. one call per tile of a frame; concurrent calls take different buffers) */
+  OutBuf buf{nullptr, 0};
+  const size_t bytes = (size_t)w * h * 16 + 16;
   hrt_status st = hguard([&] {
     DeviceGuard dg(s->device);
-    hip_check(hipMalloc((void**)&d_out, (size_t)w * h * 16 + 16), "hipMalloc(out)");
+    buf = out_pool_take(s, bytes);
   });
   if (st != HRT_OK) return st;
   hrt_render_stats local;
-  st = hrt_render_device(s, cam, p, x0, y0, w, h, d_out, nullptr, stats ? stats : &local);
+  st = hrt_render_device(s, cam, p, x0, y0, w, h, (float*)buf.ptr, nullptr, stats ? stats : &local);
   if (st == HRT_OK) {
     st = hguard([&] {
       DeviceGuard dg(s->device);
-      hip_check(hipMemcpy(rgba_out, d_out, (size_t)w * h * 16, hipMemcpyDeviceToHost), "hipMemcpy(out)");
+      hip_check(hipMemcpy(rgba_out, buf.ptr, (size_t)w * h * 16, hipMemcpyDeviceToHost), "hipMemcpy(out)");
     });
   }
-  {
-    int prev = -1;
-    (void)hipGetDevice(&prev);
-    (void)hipSetDevice(s->device);
-    (void)hipFree(d_out);
-    if (prev >= 0) (void)hipSetDevice(prev);
-  }
+  out_pool_give(s, buf);
   return st;
 }
 

@@ -147,6 +147,7 @@ struct hrt_scene {
   Slot slots[N_SLOTS];
   unsigned next_slot = 0;
   void* slot_mutex = nullptr; /* std::mutex*, owned by render.hip */
+  void* out_pool = nullptr;   /* hrt_render's reusable device output buffers (render.hip OutPool) */
 };
 
 namespace hrt {

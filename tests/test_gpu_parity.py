@@ -318,3 +318,20 @@ def test_image_size_range_is_enforced(earth):
     img = hrt.render(s, cam, hrt.params(65535, 2, 1, 4, 1, tuple(s.info.background)), region=(65000, 0, 16, 2))
     ref, _ = O.OracleScene(0, 1, earth).render(65535, 2, 1, 4, seed=1, region=(65000, 0, 16, 2))
     assert np.abs(img - ref).max() <= TOL
+
+
+@pytest.mark.gpu
+def test_hrt_render_tile_by_tile(earth):
+    """INTEGRATION.md section 3's simple loop: one synchronous hrt_render per 80x80 tile (its device
+    output buffer comes from the scene's pool, not a hipMalloc per call) reassembles the whole-frame
+    render bit for bit, buffers of different sizes included."""
+    s = hrt.preset("random", 1, earth)
+    s.commit()
+    W, H = 400, 225
+    cam = hrt.preset_camera(s.info, W, H)
+    p = hrt.params(W, H, 4, 50, 2, tuple(s.info.background))
+    full = hrt.render(s, cam, p)
+    frame = np.full((H, W, 4), np.nan, np.float32)
+    for x, y, w, h in hrt.tile_grid(W, H, 80):
+        frame[y:y + h, x:x + w] = hrt.render(s, cam, p, region=(x, y, w, h))
+    assert np.array_equal(frame, full)
