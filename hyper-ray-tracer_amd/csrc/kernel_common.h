@@ -70,10 +70,12 @@ __device__ __forceinline__ void stage_scene(const KParams& P, float4* lds, const
   prims = reinterpret_cast<const G::Prim*>(lds + n4);
 }
 
-/* A lane's current work item: one pixel and a chunk [sample, sample_end) of its samples. */
+/* A lane's current work item: one pixel and a chunk [sample, sample_end) of its samples.  slot: where
+ * the chunk's result goes, P.out[slot] (one chunk) or P.partial[slot] = [chunk][n_out] (the host checks
+ * n_chunks x n_out < 2^32); the chunk is first iff sample_end <= P.chunk. */
 struct Item {
   uint32_t pxy; /* px | py << 16 */
-  uint32_t out_idx, chunk, sample, sample_end;
+  uint32_t slot, sample, sample_end;
 };
 
 /* Idle lanes of the wave claim work items with ONE atomicAdd (ballot + popcount).  Items are
@@ -109,8 +111,7 @@ __device__ __forceinline__ void claim_work(const KParams& P, uint32_t lane, bool
   if (lx < T.w && ly < T.h) {
     has_item = true;
     it.pxy = (T.x + lx) | ((T.y + ly) << 16);
-    it.out_idx = T.out_off + ly * T.w + lx;
-    it.chunk = c;
+    it.slot = c * P.n_out + T.out_off + ly * T.w + lx;
     it.sample = c * P.chunk;
     it.sample_end = min(P.spp, it.sample + P.chunk);
   }
@@ -124,11 +125,11 @@ __device__ __forceinline__ void finish_sample(const KParams& P, Item& it, Vec3& 
   n_samples++;
   if (++it.sample == it.sample_end) {
     if (P.n_chunks == 1) {
-      P.out[it.out_idx] = make_float4(sqrtf(sum.x * scale), sqrtf(sum.y * scale), sqrtf(sum.z * scale), 1.0f);
+      P.out[it.slot] = make_float4(sqrtf(sum.x * scale), sqrtf(sum.y * scale), sqrtf(sum.z * scale), 1.0f);
       n_pixels++;
     } else {
-      P.partial[(size_t)it.chunk * P.n_out + it.out_idx] = make_float4(sum.x, sum.y, sum.z, 0.0f);
-      if (it.chunk == 0) n_pixels++;
+      P.partial[it.slot] = make_float4(sum.x, sum.y, sum.z, 0.0f);
+      if (it.sample_end <= P.chunk) n_pixels++;
     }
     has_item = false;
     sum = v3(0.0f, 0.0f, 0.0f);

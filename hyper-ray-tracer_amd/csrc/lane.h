@@ -77,6 +77,7 @@ struct KParams {
   uint32_t walk_bytes; /* whole stream */
   uint32_t walk_end;   /* byte offset one past the last record */
   uint32_t walk_hot;   /* WM_HYB: offsets below this are staged in LDS (layout.h placement) */
+  uint32_t lane_lds;   /* sphere kernel: LDS byte offset of the per-lane result slots (after the staged scene) */
 };
 
 /* per-lane work counters of the instrumented (COUNT) instantiation */

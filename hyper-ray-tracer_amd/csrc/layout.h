@@ -178,8 +178,10 @@ constexpr uint32_t KIND_MASK = 0x7Fu;
  * parts of the hierarchy's top levels first (breadth first, up to LDS_SCENE_MAX_BYTES: the bytes the
  * kernel stages in LDS, w_hot), then everything else in pre-order in global memory. */
 constexpr uint32_t WALK_PEND = 1u << 31;
-/* the largest scene a sphere-kernel workgroup stages in LDS: two workgroups per CU share its 160 KiB */
-constexpr uint32_t LDS_SCENE_MAX_BYTES = 78u * 1024u;
+/* the largest scene a sphere-kernel workgroup stages in LDS: two workgroups per CU share its 160 KiB,
+ * each also holding a u32 result slot for each of its (at most 768) threads */
+constexpr uint32_t LDS_SCENE_MAX_BYTES = 77u * 1024u;
+static_assert(2u * (LDS_SCENE_MAX_BYTES + 768u * 4u) <= 160u * 1024u, "two sphere workgroups per CU");
 constexpr uint32_t WALK_NODE_BYTES = 32, WALK_PAYLOAD_BYTES = 96;
 constexpr uint32_t WL_MOVING = 1u, WL_NOBOX = 2u;
 enum : uint32_t { WT_SOLID = 0, WT_CHECKER = 1, WT_GLOBAL = 2 }; /* inline texture of a leaf's material */

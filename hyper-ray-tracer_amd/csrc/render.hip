@@ -88,7 +88,7 @@ void render_kernel(KParams P) {
   const float scale = 1.0f / (float)P.spp; /* application.rs:403 */
 
   bool has_item = false, exhausted = false, in_path = false;
-  Item it{0u, 0u, 0u, 0u, 0u};
+  Item it{0u, 0u, 0u, 0u};
   Vec3 sum = v3(0.0f, 0.0f, 0.0f);
   PathState ps;
   init_path_state(ps);
@@ -137,7 +137,7 @@ void render_full_kernel(KParams P) {
 
   bool has_item = false, exhausted = false;
   bool walking = false;
-  Item it{0u, 0u, 0u, 0u, 0u};
+  Item it{0u, 0u, 0u, 0u};
   Vec3 sum = v3(0.0f, 0.0f, 0.0f);
   PathState ps;
   init_path_state(ps);
@@ -206,11 +206,11 @@ void render_full_kernel(KParams P) {
         w.end = 0u;
         sum = sum + ps.rad;
         sample_done = true;
-        if (++it.sample == min(P.spp, (it.chunk + 1u) * P.chunk)) {
+        if (++it.sample == it.sample_end) {
           if (P.n_chunks == 1)
-            P.out[it.out_idx] = make_float4(sqrtf(sum.x * scale), sqrtf(sum.y * scale), sqrtf(sum.z * scale), 1.0f);
+            P.out[it.slot] = make_float4(sqrtf(sum.x * scale), sqrtf(sum.y * scale), sqrtf(sum.z * scale), 1.0f);
           else
-            P.partial[(size_t)it.chunk * P.n_out + it.out_idx] = make_float4(sum.x, sum.y, sum.z, 0.0f);
+            P.partial[it.slot] = make_float4(sum.x, sum.y, sum.z, 0.0f);
           chunk_done = true;
           has_item = false;
           sum = v3(0.0f, 0.0f, 0.0f);
@@ -222,7 +222,7 @@ void render_full_kernel(KParams P) {
     }
     n_seg += (uint32_t)__popcll(__ballot(traced));
     n_samples += (uint32_t)__popcll(__ballot(sample_done));
-    n_pixels += (uint32_t)__popcll(__ballot(chunk_done && it.chunk == 0u));
+    n_pixels += (uint32_t)__popcll(__ballot(chunk_done && it.sample_end <= P.chunk));
   }
   if (lane == 0) {
     atomicAdd(&P.stats[0], (unsigned long long)n_seg);
@@ -655,7 +655,8 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
       pad += (uint64_t)bw * bh * 64 * n_chunks;
       outp += (uint64_t)t.w * t.h;
     }
-    if (pad >= 0xFFFF0000ull) throw HipError{HRT_ERR_UNSUPPORTED, "more than 4G pixels in one call"};
+    /* work items and Item.slot (chunk x n_out + pixel <= pad) are 32-bit */
+    if (pad >= 0xFFFF0000ull) throw HipError{HRT_ERR_UNSUPPORTED, "more than 4G pixel x sample-chunk items in one call"};
     hipStream_t stream = (hipStream_t)stream_;
     DeviceGuard dg(s->device);
     /* scratch slot: device [counter u32 | pad | stats 8 x u64 | pad to HDR | tiles], pinned host [stats | tiles] */

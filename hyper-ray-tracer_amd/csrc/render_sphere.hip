@@ -46,6 +46,9 @@ void render_basic_kernel(KParams P) {
   } else if constexpr (LDS) {
     stage_scene<true>(P, lds_scene, nodes, prims, root);
   }
+  /* the lane's Item.slot lives in LDS: a register kept across the whole item would be spilled at the
+   * 80-VGPR cap (scratch written at every claim and chunk end) */
+  uint32_t* const slot_lds = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(lds_scene) + P.lane_lds) + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63u;
   const float scale = 1.0f / (float)P.spp; /* application.rs:403 */
   const float inf = __uint_as_float(0x7f800000u);
@@ -60,7 +63,7 @@ void render_basic_kernel(KParams P) {
 
   bool has_item = false, exhausted = false;
   bool walking = false; /* a segment is in flight (walk running, or finished and waiting to shade) */
-  Item it{0u, 0u, 0u, 0u, 0u};
+  Item it{0u, 0u, 0u, 0u};
   Vec3 sum = v3(0.0f, 0.0f, 0.0f);
   PathState ps;
   init_path_state(ps);
@@ -82,7 +85,9 @@ void render_basic_kernel(KParams P) {
 
   for (;;) {
     /* lanes without work claim it; lanes with work but no segment in flight start a sample */
+    const bool had_item = has_item;
     claim_work(P, lane, has_item, exhausted, it);
+    if (has_item && !had_item) *slot_lds = it.slot;
     if (!__any(has_item || !exhausted)) break;
     if (has_item && !walking) {
       start_sample(P, ps, it.pxy & 0xFFFFu, it.pxy >> 16, it.sample);
@@ -148,11 +153,11 @@ void render_basic_kernel(KParams P) {
         node = G::NONE;
         sum = sum + ps.rad;
         sample_done = true;
-        if (++it.sample == min(P.spp, (it.chunk + 1u) * P.chunk)) {
+        if (++it.sample == it.sample_end) {
           if (P.n_chunks == 1) /* sqrt(sum / spp), alpha 1 (:451-456) */
-            P.out[it.out_idx] = make_float4(sqrtf(sum.x * scale), sqrtf(sum.y * scale), sqrtf(sum.z * scale), 1.0f);
+            P.out[*slot_lds] = make_float4(sqrtf(sum.x * scale), sqrtf(sum.y * scale), sqrtf(sum.z * scale), 1.0f);
           else
-            P.partial[(size_t)it.chunk * P.n_out + it.out_idx] = make_float4(sum.x, sum.y, sum.z, 0.0f);
+            P.partial[*slot_lds] = make_float4(sum.x, sum.y, sum.z, 0.0f);
           chunk_done = true;
           has_item = false;
           sum = v3(0.0f, 0.0f, 0.0f);
@@ -166,7 +171,7 @@ void render_basic_kernel(KParams P) {
     }
     n_seg += (uint32_t)__popcll(__ballot(traced));
     n_samples += (uint32_t)__popcll(__ballot(sample_done));
-    n_pixels += (uint32_t)__popcll(__ballot(chunk_done && it.chunk == 0u));
+    n_pixels += (uint32_t)__popcll(__ballot(chunk_done && it.sample_end <= P.chunk));
     stamp(2);
   }
   if (lane == 0) {
@@ -186,8 +191,13 @@ template <int CULL, bool COUNT, bool LDS, bool HYB = false>
 void launch_basic(const KParams& kp, int device, hipStream_t stream, size_t smem) {
   const void* fn = (const void*)render_basic_kernel<CULL, COUNT, LDS, HYB>;
   const int block = basic_block_threads<LDS>();
-  const int grid = resident_grid(fn, block, device, LDS ? smem : 0, LDS);
-  hipLaunchKernelGGL((render_basic_kernel<CULL, COUNT, LDS, HYB>), dim3(grid), dim3(block), LDS ? smem : 0, stream, kp);
+  /* LDS: the staged scene, then one u32 result slot per thread (layout.h LDS_SCENE_MAX_BYTES leaves
+   * room for both, twice per CU) */
+  KParams p = kp;
+  p.lane_lds = LDS ? (uint32_t)((smem + 15) & ~(size_t)15) : 0u;
+  const size_t total = p.lane_lds + (size_t)block * sizeof(uint32_t);
+  const int grid = resident_grid(fn, block, device, total, true);
+  hipLaunchKernelGGL((render_basic_kernel<CULL, COUNT, LDS, HYB>), dim3(grid), dim3(block), total, stream, p);
   hip_check(hipGetLastError(), "render_basic_kernel launch");
 }
 
