@@ -144,6 +144,8 @@ __device__ __forceinline__ void flush_counts(const KParams& P, const Counts& cn)
   atomicAdd(&P.stats[6], (unsigned long long)cn.walk_slots);
   atomicAdd(&P.stats[7], (unsigned long long)cn.shade_slots);
   atomicAdd(&P.stats[8], (unsigned long long)cn.prim_slots);
+  atomicAdd(&P.stats[13], (unsigned long long)cn.park_slots);
+  atomicAdd(&P.stats[14], (unsigned long long)cn.wait_slots);
 }
 
 __device__ __forceinline__ void flush_stats(const KParams& P, uint32_t n_seg, uint32_t n_samples, uint32_t n_pixels,

@@ -85,6 +85,7 @@ struct Counts {
   uint32_t nodes, prims, tex;
   uint32_t walk_slots, shade_slots; /* lane slots of wave iterations: walk (node) loop, shading passes */
   uint32_t prim_slots;              /* lane slots of wave executions of the primitive block */
+  uint32_t park_slots, wait_slots;  /* sphere kernel walk steps: lanes parked on a leaf / done, waiting to shade */
 };
 
 struct TRay {
@@ -1082,12 +1083,10 @@ HRT_LANE_FI void walk_box(const WalkSrc& src, uint32_t& i, const TRay& r, float 
 /* The parked leaf's primitive: the reference test on its box (aabb.rs, monotone: leaves suffice, DESIGN
  * section 4), then the sphere test against the lane's closest; the walk continues behind the leaf. */
 template <bool COUNT, int MEM>
-HRT_LANE_FI void walk_prim(const KParams& P, const WalkSrc& src, uint32_t& i, const TRay& r, float& closest,
-                           uint32_t& winner, Counts& cn) {
-  const uint32_t leaf = i - WALK_PEND; /* the leaf's payload */
+HRT_LANE_FI void walk_leaf_test(const KParams& P, const WalkSrc& src, uint32_t leaf, const TRay& r, float& closest,
+                                uint32_t& winner, Counts& cn) {
   const float4 bmn = wload<MEM>(src, leaf), bmx = wload<MEM>(src, leaf + 16u);
   const uint32_t w = f2u(bmn.w);
-  i = w >> 2; /* the walk goes on at the leaf's pre-order successor */
   if (!(w & G::WL_NOBOX) && !box_ref(bmn, bmx, r, P.t_min, closest)) return;
   if constexpr (COUNT) cn.prims++;
   const float4 s0 = wload<MEM>(src, leaf + 32u);
@@ -1102,6 +1101,18 @@ HRT_LANE_FI void walk_prim(const KParams& P, const WalkSrc& src, uint32_t& i, co
     closest = t;
     winner = leaf; /* shade_walk reads the sphere and its material from the leaf */
   }
+}
+
+/* the leaf's pre-order successor, kept in its payload (w >> 2) */
+template <int MEM>
+HRT_LANE_FI uint32_t walk_successor(const WalkSrc& src, uint32_t leaf) { return f2u(wload<MEM>(src, leaf).w) >> 2; }
+
+template <bool COUNT, int MEM>
+HRT_LANE_FI void walk_prim(const KParams& P, const WalkSrc& src, uint32_t& i, const TRay& r, float& closest,
+                           uint32_t& winner, Counts& cn) {
+  const uint32_t leaf = i - WALK_PEND; /* the leaf's payload */
+  i = walk_successor<MEM>(src, leaf); /* the walk goes on at the leaf's pre-order successor */
+  walk_leaf_test<COUNT, MEM>(P, src, leaf, r, closest, winner, cn);
 }
 
 /* both halves back to back (the host lane simulator's walk) */

@@ -294,7 +294,7 @@ hrt_status hguard(F&& f) {
   }
 }
 
-constexpr size_t SLOT_HDR = 128; /* work counter + 12 stats words + error word, padded */
+constexpr size_t SLOT_HDR = 128; /* work counter (8 B), stats words 0-11, error word 12, stats words 13-14 */
 
 constexpr const char* SLOT_ERROR_MSG =
     "a render launch on this scene stopped walks that did not terminate (corrupt scene data); its frame is incomplete";
@@ -474,8 +474,11 @@ KParams scene_params(const hrt_scene* s, const hrt_camera* cam, const hrt_render
   kp.n_nodes = pl.fast ? 8 * s->f_stream_len : (uint32_t)s->g_nodes.size(); /* main stream + medium boundary subtrees */
   kp.n_prims = (uint32_t)(pl.fast ? s->f_prims.size() : s->g_prims.size());
   kp.stream_len = pl.fast ? s->f_stream_len : 0;
-  kp.postpone = env_knob("HRT_POSTPONE", 56);
-  kp.prim_batch = env_knob("HRT_PRIM_BATCH", 8);
+  /* the sphere kernel's speculative walk (render_sphere.hip SPEC) blocks lanes less often: it runs best
+   * with smaller batches (sweep on C2) */
+  const bool spec = !pl.full && !pl.general && !pl.fast && pl.cull == G::CULL_EXACT;
+  kp.postpone = env_knob("HRT_POSTPONE", spec ? 48 : 56);
+  kp.prim_batch = env_knob("HRT_PRIM_BATCH", spec ? 6 : 8);
   /* a walk visits each node at most once, a medium's boundary subtree at most twice per medium node */
   kp.walk_cap = 3u * (uint32_t)s->g_nodes.size() + 64u;
   kp.motion_uniform = s->motion_uniform ? 1u : 0u;
@@ -717,7 +720,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     /* the stats words and the watchdog's error word (h[12]) come back after EVERY launch, so a killed
      * frame is reported even when the caller asked for no stats (take_slot_error) */
     unsigned long long* h = (unsigned long long*)sl.h_tiles;
-    hip_check(hipMemcpyAsync(h, (uint8_t*)scratch + 8, 104, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(stats)");
+    hip_check(hipMemcpyAsync(h, (uint8_t*)scratch + 8, 120, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(stats)");
     hip_check(hipEventRecord((hipEvent_t)sl.event, stream), "hipEventRecord(slot)");
     sl.used = true;
     if (stats) {
@@ -733,6 +736,8 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
       stats->shade_slots = h[7];
       stats->prim_slots = h[8];
       for (int k = 0; k < 3; k++) stats->phase_cycles[k] = h[9 + k];
+      stats->park_slots = h[13];
+      stats->wait_slots = h[14];
     }
   });
 }

@@ -10,6 +10,10 @@ using namespace hrt;
 using namespace hrt::lane;
 using namespace hrt::kern;
 
+#ifndef HRT_SPEC
+#define HRT_SPEC 1 /* speculative walk of the walk stream (0: lanes park on every passed leaf, for A/B) */
+#endif
+
 namespace {
 
 /* HYB (CULL_EXACT with LDS): the walk stream exceeds the LDS budget; its first P.walk_hot bytes (the
@@ -24,6 +28,7 @@ void render_basic_kernel(KParams P) {
    * descriptor); the other modes walk the reference node stream (with the scene in LDS the walk
    * position is the node's LDS byte address, basic_box STRIDE) */
   constexpr bool WS = CULL == G::CULL_EXACT;
+  constexpr bool SPEC = WS && HRT_SPEC;
   constexpr int WMEM = HYB ? WM_HYB : (LDS ? WM_LDS : WM_BUF);
   constexpr uint32_t STRIDE = LDS ? (uint32_t)sizeof(G::Node) : 1u;
   const uint32_t lds_base = (uint32_t)(size_t)(__attribute__((address_space(3))) float4*)lds_scene;
@@ -70,6 +75,11 @@ void render_basic_kernel(KParams P) {
   TRay r;
   set_ray(r, ps.ro, ps.rd, 0.0f, P);
   uint32_t node = G::NONE, winner = G::NONE; /* node: walk position (basic_box: index | WALK_PEND, or NONE) */
+  /* SPEC: a passed leaf whose test waits for the wave's next primitive block while the lane walks on
+   * (speculative traversal: the walk runs ahead with a closest that the pending test may still shrink,
+   * so it visits a superset of the nodes; the leaf tests, each with the reference box test against the
+   * current closest, keep their order and outcomes: DESIGN.md section 4) */
+  uint32_t pend = G::NONE;
   float closest = inf;
   uint32_t n_seg = 0, n_samples = 0, n_pixels = 0; /* wave totals (uniform) */
   Counts cn{0u, 0u, 0u, 0u, 0u, 0u};
@@ -112,8 +122,33 @@ void render_basic_kernel(KParams P) {
         if (node < end) {
           if constexpr (WS) walk_box<COUNT, WMEM>(ws, node, r, tmin_c, closest, cn);
           else basic_box<CULL, COUNT, STRIDE>(P, nodes, node, r, closest, cn);
+        } else if constexpr (COUNT) {
+          if (walk_pending(node)) cn.park_slots++;
+          else if (walking) cn.wait_slots++;
         }
         if ((u + 1) % PRIM_EVERY != 0) continue;
+        if constexpr (SPEC) {
+          /* a lane parked on a leaf with no test pending makes the leaf's test pending and walks on behind
+           * it; a lane parks for good (blocked) only on a second leaf, or at the end of its walk */
+          if (walk_pending(node) && pend == G::NONE) {
+            pend = node - WALK_PEND;
+            node = walk_successor<WMEM>(ws, pend);
+          }
+          const bool waiting = pend != G::NONE && !(node < end);
+          const unsigned long long pm = __ballot(waiting);
+          if (pm && ((uint32_t)__popcll(pm) >= batch || !__ballot(node < end))) {
+            if constexpr (COUNT) cn.prim_slots++;
+            if (pend != G::NONE) { /* the pending tests of every lane, walking or blocked, in walk order */
+              walk_leaf_test<COUNT, WMEM>(P, ws, pend, r, closest, winner, cn);
+              pend = G::NONE;
+              if (walk_pending(node)) { /* blocked: its leaf's test becomes the pending one */
+                pend = node - WALK_PEND;
+                node = walk_successor<WMEM>(ws, pend);
+              }
+            }
+          }
+          continue;
+        }
         const bool waiting = walk_pending(node);
         const unsigned long long pm = __ballot(waiting);
         if (pm && ((uint32_t)__popcll(pm) >= batch || !__ballot(node < end))) {
@@ -124,7 +159,7 @@ void render_basic_kernel(KParams P) {
           }
         }
       }
-      const unsigned long long live = __ballot(node < end || walk_pending(node));
+      const unsigned long long live = __ballot(node < end || walk_pending(node) || (SPEC && pend != G::NONE));
       if (!live || (uint32_t)__popcll(walkers & ~live) >= need) break;
       if (++iters > cap) { stuck = true; break; }
     }
@@ -134,10 +169,11 @@ void render_basic_kernel(KParams P) {
       has_item = false;
       walking = false;
       node = G::NONE;
+      pend = G::NONE;
     }
     stamp(1);
     /* shade the finished segments (application.rs:483-494) */
-    const bool shading = walking && node >= end && !walk_pending(node);
+    const bool shading = walking && node >= end && !walk_pending(node) && (!SPEC || pend == G::NONE);
     const bool traced = shading && node != G::NONE;
     bool sample_done = false, chunk_done = false;
     if (shading) {

@@ -116,6 +116,9 @@ typedef struct hrt_render_stats {
                                (sphere-scene kernel; 0 for the general kernel) */
   uint64_t phase_cycles[3]; /* HRT_RENDER_COUNT_WORK, sphere-scene kernel: shader cycles summed over
                                waves spent in [0] work claim + sample start, [1] walk, [2] shading */
+  uint64_t park_slots;      /* HRT_RENDER_COUNT_WORK, sphere-scene kernel: lane slots of walk steps spent parked on
+                               a leaf (waiting for the batched primitive test) */
+  uint64_t wait_slots;      /* ... spent with the walk done, waiting for the wave to leave the walk and shade */
 } hrt_render_stats;
 
 /* Scene description of one reference preset (application.rs:132-211). */

@@ -75,5 +75,10 @@ for key in flag_sets:
         pcs = list(st.phase_cycles)
         if sum(pcs):
             print("   phase cycles: claim+start {:.1%}  walk {:.1%}  shade {:.1%}".format(*[c / sum(pcs) for c in pcs]), flush=True)
+        if st.walk_slots:
+            ws = st.walk_slots
+            print(f"   walk slots: stepping {st.node_visits/ws:.1%}  parked on a leaf {st.park_slots/ws:.1%}  "
+                  f"done, waiting to shade {st.wait_slots/ws:.1%}  no walk {1 - (st.node_visits + st.park_slots + st.wait_slots)/ws:.1%}",
+                  flush=True)
 img = out.cpu().numpy()
 print("mean rgb", img[..., :3].mean(axis=(0, 1)), "finite", bool(np.isfinite(img).all()))
