@@ -845,8 +845,9 @@ HRT_LANE_FI bool scatter(PathState& ps, const Rec& rec, uint32_t kind, Vec3 albe
     if (FULL && kind == G::M_DIFFUSE_LIGHT) emitted = tv;
     else att = tv;
   }
-  /* L = emitted + att * L_next, accumulated front to back */
-  ps.rad = ps.rad + mul_elem(ps.thr, emitted);
+  /* L = emitted + att * L_next, accumulated front to back (only FULL scenes have emitters: without
+   * them rad stays +0 until the path's miss, and adding thr x 0 would change no bit) */
+  if constexpr (FULL) ps.rad = ps.rad + mul_elem(ps.thr, emitted);
   if (!scattered) return true;
   ps.thr = mul_elem(ps.thr, att);
   ps.ro = rec.p;
@@ -875,9 +876,10 @@ HRT_LANE_FI bool shade(const KParams& P, PathState& ps, uint32_t winner, float c
  * sphere and its material, so the hit record and the scatter read the walk stream only (LDS). */
 template <bool COUNT, int MEM>
 HRT_LANE_FI bool shade_walk(const KParams& P, const WalkSrc& src, PathState& ps, uint32_t leaf, float closest,
-                            Vec3 ro, Vec3 rd, float rtime, float tau, Counts& cn) {
-  if (leaf == G::NONE) {
-    ps.rad = ps.rad + mul_elem(ps.thr, P.background);
+                            Vec3 ro, Vec3 rd, float rtime, float tau, Vec3& sum, Counts& cn) {
+  if (leaf == G::NONE) { /* a sphere scene's path gathers radiance at its miss only: straight into the sum
+                          * (sum + (+0 + thr bg) == sum + thr bg: the sum is never -0) */
+    sum = sum + mul_elem(ps.thr, P.background);
     return true;
   }
   /* sphere.rs:57-73 / moving_sphere.rs:80-94 (leaf = the winning leaf's payload) */

@@ -179,7 +179,7 @@ void render_basic_kernel(KParams P) {
     if (shading) {
       bool done = true;
       if (traced) {
-        if constexpr (WS) done = shade_walk<COUNT, WMEM>(P, ws, ps, winner, closest, r.o, r.d, r.time, r.tau, cn);
+        if constexpr (WS) done = shade_walk<COUNT, WMEM>(P, ws, ps, winner, closest, r.o, r.d, r.time, r.tau, sum, cn);
         else done = shade<false, COUNT>(P, ps, winner, closest, r.o, r.d, r.time, r.tau, cn);
         done = done || ps.depth_left == 0;
       }
@@ -187,7 +187,7 @@ void render_basic_kernel(KParams P) {
         /* application.rs:448: samples of a chunk summed in order */
         walking = false;
         node = G::NONE;
-        sum = sum + ps.rad;
+        if constexpr (!WS) sum = sum + ps.rad; /* shade_walk added a miss's radiance already */
         sample_done = true;
         if (++it.sample == it.sample_end) {
           if (P.n_chunks == 1) /* sqrt(sum / spp), alpha 1 (:451-456) */

@@ -77,7 +77,7 @@ void render_pixel(const KParams& P, uint32_t px, uint32_t py, float* rgba, uint6
           if constexpr (CULL == G::CULL_EXACT) {
             WalkSrc src;
             src.base = P.walk;
-            done = !traced || shade_walk<true, WM_HOST>(P, src, ps, winner, closest, r.o, r.d, r.time, r.tau, cn) ||
+            done = !traced || shade_walk<true, WM_HOST>(P, src, ps, winner, closest, r.o, r.d, r.time, r.tau, sum, cn) ||
                    ps.depth_left == 0;
           } else {
             done = !traced ||
