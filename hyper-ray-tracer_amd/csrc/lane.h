@@ -1035,13 +1035,12 @@ HRT_LANE_FI void basic_step(const KParams& P, const G::Node* __restrict__ nodes,
 /* The inflated test of CULL_EXACT on a box given by centre C and half-extent E (the walk stream's inner
  * boxes, which hold the reference boxes): false only if the box, widened by EXACT_MARGIN x D' (D' =
  * max_k |C_k - o_k| + E_k >= the L-inf distance of its farthest point from the origin), misses the ray
- * on [tmin, tmax].  Per axis the slab is m_k -+ E_k |inv_k| with m_k = (C_k - o_k) inv_k, so the
- * near/far swap of aabb.rs:28-29 disappears; half-extent and widening are one product,
- * w_k = (E_k + EXACT_MARGIN D') |inv_k| (an fma and a multiply, nothing per ray beyond 1/d).  Rounding
- * errors of the whole computation stay below ~6 2^-24 D' |inv_k|, far inside the slack of
- * EXACT_MARGIN (layout.h: 4e-3 covers the 2.4e-3 needed 1.65 times).  A NaN bound
- * (inv_k = +-inf: C_k = o_k or E_k = 0) is ignored by max3/min3: no constraint.  An infinite box
- * (E = +inf) always passes. */
+ * on [tmin, tmax].  Per axis the slab is m_k -+ t_k |inv_k| with m_k = (C_k - o_k) inv_k and
+ * t_k = E_k + EXACT_MARGIN D', so the near/far swap of aabb.rs:28-29 disappears; each bound is one fma
+ * (t_k by fmamk, the bounds by fma with |inv_k| as a source modifier: 21 VALU per box).  Rounding errors
+ * of the whole computation stay below ~6 2^-24 D' |inv_k|, far inside the slack of EXACT_MARGIN
+ * (layout.h: 4e-3 covers the 2.4e-3 needed 1.65 times).  A NaN bound (inv_k = +-inf: C_k = o_k or
+ * E_k = 0) is ignored by max3/min3: no constraint.  An infinite box (E = +inf) always passes. */
 HRT_LANE_FI bool box_ce(const float4& a, const float4& b, const TRay& r, float tmin, float tmax) {
   const float C[3] = {a.x, a.y, a.z}, E[3] = {b.x, b.y, b.z};
   const float o[3] = {r.o.x, r.o.y, r.o.z}, inv[3] = {r.inv.x, r.inv.y, r.inv.z};
@@ -1057,13 +1056,16 @@ HRT_LANE_FI bool box_ce(const float4& a, const float4& b, const TRay& r, float t
     m[k] = dc * inv[k];
     e[k] = fabsf(dc) + E[k];
   }
+  /* the farthest point's distance per axis: monotone under box inclusion, so a child's inflated box
+   * lies in its parent's and every hierarchy over the same leaves tests the same leaves (max |dc| +
+   * max E would save an instruction but is not monotone) */
   const float dist = fmaxf(fmaxf(e[0], e[1]), e[2]);
   float l[3], h[3];
 #pragma unroll
   for (int k = 0; k < 3; k++) {
-    const float w = fmaf(dist, G::EXACT_MARGIN, E[k]) * fabsf(inv[k]);
-    l[k] = m[k] - w;
-    h[k] = m[k] + w;
+    const float t = fmaf(dist, G::EXACT_MARGIN, E[k]);
+    l[k] = fmaf(-t, fabsf(inv[k]), m[k]);
+    h[k] = fmaf(t, fabsf(inv[k]), m[k]);
   }
   const float lo = fmaxf(fmaxf(l[0], l[1]), l[2]); /* NaN only if all three are: no constraint */
   const float hi = fminf(fminf(h[0], h[1]), h[2]);
