@@ -1079,6 +1079,9 @@ HRT_LANE_FI void walk_box(const WalkSrc& src, uint32_t& i, const TRay& r, float 
   uint32_t skip = f2u(a.w);
 #if defined(__HIP_DEVICE_COMPILE__)
   asm("" : "+v"(skip)); /* keep the link in the first 16-B load (see basic_box) */
+#if HRT_EXP_LDS2 /* timing experiment: one more 16-B LDS read per step (is the walk LDS-bound?) */
+  { const float4 x = wload<MEM>(src, i + 32u); asm volatile("" :: "v"(x.x), "v"(x.y), "v"(x.z), "v"(x.w)); }
+#endif
 #endif
   if constexpr (COUNT) cn.nodes++;
   i = box_ce(a, b, r, tmin, closest) ? f2u(b.w) : skip;

@@ -68,6 +68,7 @@ void render_basic_kernel(KParams P) {
 
   bool has_item = false, exhausted = false;
   bool walking = false; /* a segment is in flight (walk running, or finished and waiting to shade) */
+  bool setup = false;   /* the lane's next segment needs its ray set up (a new sample, or a scattered ray) */
   Item it{0u, 0u, 0u, 0u};
   Vec3 sum = v3(0.0f, 0.0f, 0.0f);
   PathState ps;
@@ -102,10 +103,14 @@ void render_basic_kernel(KParams P) {
     if (has_item && !walking) {
       start_sample(P, ps, it.pxy & 0xFFFFu, it.pxy >> 16, it.sample);
       walking = true;
-      set_ray(r, ps.ro, ps.rd, ps.rtime, P);
+      setup = true;
+    }
+    if (setup) { /* new samples and scattered rays share one pass through the ray setup (1/d, d.d) */
+      set_ray(r, ps.ro, ps.rd, ps.rtime, P); /* a scattered ray keeps the sample's shutter time */
       closest = inf;
       winner = G::NONE;
       node = ps.depth_left == 0 ? G::NONE : root; /* max_depth 0: black without a world.hit (:478-480) */
+      setup = false;
     }
     /* step the walks until enough lanes have finished (lanes not walking hold node >= end).  A lane
      * whose leaf box passed holds WALK_PEND in `node` and waits; the wave runs the sphere block
@@ -199,10 +204,8 @@ void render_basic_kernel(KParams P) {
           sum = v3(0.0f, 0.0f, 0.0f);
         }
       } else {
-        set_dir(r, ps.ro, ps.rd); /* the scattered ray keeps the sample's shutter time */
-        closest = inf;
-        winner = G::NONE;
-        node = root;
+        setup = true; /* the scattered ray (depth_left > 0) is set up with the next pass's new samples */
+        node = G::NONE;
       }
     }
     n_seg += (uint32_t)__popcll(__ballot(traced));
