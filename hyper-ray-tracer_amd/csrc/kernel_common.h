@@ -78,21 +78,41 @@ struct Item {
   uint32_t slot, sample, sample_end;
 };
 
-/* Idle lanes of the wave claim work items with ONE atomicAdd (ballot + popcount).  Items are
- * ordered [tile][8x8 block][chunk][64 pixels], so a wave starts on 64 neighbouring pixels. */
+/* Work items claimed by a wave and not yet handed to a lane: [next, end) (wave-uniform). */
+struct WaveBlock {
+  uint32_t next, end;
+};
+constexpr uint32_t CLAIM_BLOCK = 64; /* items per atomicAdd on the work counter */
+
+/* Idle lanes of the wave take work items from the wave's block (ballot + popcount); when it runs short
+ * the wave claims the next CLAIM_BLOCK items with ONE atomicAdd.  Items are ordered [tile][8x8 block]
+ * [chunk][64 pixels], so a block is one chunk of 64 neighbouring pixels.  A wave hands out its whole
+ * block before it claims another, and its lanes retire only on an item past the end, so no item is
+ * left behind. */
 __device__ __forceinline__ void claim_work(const KParams& P, uint32_t lane, bool& has_item, bool& exhausted,
-                                           Item& it) {
+                                           Item& it, WaveBlock& wb) {
   const bool want = !has_item && !exhausted;
   const unsigned long long want_mask = __ballot(want);
   if (!want_mask) return;
   const uint32_t cnt = (uint32_t)__popcll(want_mask);
-  const int leader = __ffsll((long long)want_mask) - 1;
-  uint32_t base = 0;
-  if ((int)lane == leader) base = atomicAdd(P.counter, cnt);
-  base = __shfl(base, leader);
-  if (!want) return;
   const uint32_t rank = (uint32_t)__popcll(want_mask & ((1ull << lane) - 1ull));
-  const uint32_t w = base + rank;
+  const uint32_t avail = wb.end - wb.next;
+  uint32_t w = wb.next + rank;
+  if (cnt > avail) { /* the block's rest, then a new block (cnt <= 64 = CLAIM_BLOCK) */
+    /* the frame's last items go one per lane again (P.claim_fine), so no wave sits on a block while
+     * other waves idle at the end */
+    const uint32_t size = wb.end >= P.claim_fine ? cnt - avail : CLAIM_BLOCK;
+    const int leader = __ffsll((long long)want_mask) - 1;
+    uint32_t base = 0;
+    if ((int)lane == leader) base = atomicAdd(P.counter, size);
+    base = __builtin_amdgcn_readfirstlane(__shfl(base, leader));
+    if (rank >= avail) w = base + (rank - avail);
+    wb.next = base + (cnt - avail);
+    wb.end = base + size;
+  } else {
+    wb.next += cnt;
+  }
+  if (!want) return;
   if (w >= P.total_work) {
     exhausted = true;
     return;

@@ -60,6 +60,7 @@ struct KParams {
   uint32_t total_work;
   float4* out;
   uint32_t* counter;
+  uint32_t claim_fine; /* work items from here on are claimed one per lane (kernel_common.h claim_work) */
   unsigned long long* stats; /* segments, samples, pixels, then (COUNT builds) nodes, prims, tex */
   /* sample chunks: a work item is (pixel, chunk of `chunk` consecutive samples) */
   uint32_t chunk, n_chunks, n_out;

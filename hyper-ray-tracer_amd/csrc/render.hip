@@ -89,6 +89,7 @@ void render_kernel(KParams P) {
 
   bool has_item = false, exhausted = false, in_path = false;
   Item it{0u, 0u, 0u, 0u};
+  WaveBlock wb{0u, 0u};
   Vec3 sum = v3(0.0f, 0.0f, 0.0f);
   PathState ps;
   init_path_state(ps);
@@ -102,7 +103,7 @@ void render_kernel(KParams P) {
       cn.shade_slots++;
       seg_nodes = 0;
     }
-    claim_work(P, lane, has_item, exhausted, it);
+    claim_work(P, lane, has_item, exhausted, it, wb);
     if (!__any(has_item || !exhausted)) break;
     if (!has_item) continue;
     if (!in_path) {
@@ -138,6 +139,7 @@ void render_full_kernel(KParams P) {
   bool has_item = false, exhausted = false;
   bool walking = false;
   Item it{0u, 0u, 0u, 0u};
+  WaveBlock wb{0u, 0u};
   Vec3 sum = v3(0.0f, 0.0f, 0.0f);
   PathState ps;
   init_path_state(ps);
@@ -160,7 +162,7 @@ void render_full_kernel(KParams P) {
   };
 
   for (;;) {
-    claim_work(P, lane, has_item, exhausted, it);
+    claim_work(P, lane, has_item, exhausted, it, wb);
     if (!__any(has_item || !exhausted)) break;
     if (has_item && !walking) {
       start_sample(P, ps, it.pxy & 0xFFFFu, it.pxy >> 16, it.sample);
@@ -659,7 +661,8 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
       outp += (uint64_t)t.w * t.h;
     }
     /* work items and Item.slot (chunk x n_out + pixel <= pad) are 32-bit */
-    if (pad >= 0xFFFF0000ull) throw HipError{HRT_ERR_UNSUPPORTED, "more than 4G pixel x sample-chunk items in one call"};
+    /* headroom: waves claim blocks of CLAIM_BLOCK items past the end before they retire */
+    if (pad >= 0xF0000000ull) throw HipError{HRT_ERR_UNSUPPORTED, "more than 3.75G pixel x sample-chunk items in one call"};
     hipStream_t stream = (hipStream_t)stream_;
     DeviceGuard dg(s->device);
     /* scratch slot: device [counter u32 | pad | stats 8 x u64 | pad to HDR | tiles], pinned host [stats | tiles] */
@@ -702,6 +705,16 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     kp.tiles = (const G::TileDev*)((uint8_t*)scratch + SLOT_HDR);
     kp.n_tiles = n_tiles;
     kp.total_work = (uint32_t)pad;
+    /* the sphere kernel claims blocks of items to the end: its passes are short, and per-lane claims
+     * made them wait on the contended counter (r02y: +12% on C2; per-lane claims for the last 0.26 /
+     * 1 / 4 M items measured +0.7 / -0.5 / -3% on C2 and -1 / -9 / -6% on a 1/8-frame share).  The
+     * segment kernels claim per lane: a segment iteration is long, claims are rare, and with few items
+     * per lane (Cornell 1024^2 x 128: 2) blocks unbalance the waves (-6%).
+     * HRT_CLAIM_FINE (A/B knob): claim the last that many items per lane, in every kernel */
+    const bool sphere_kernel = !pl.full && !pl.fast && !pl.general;
+    const char* cf = getenv("HRT_CLAIM_FINE");
+    const uint64_t fine = cf ? strtoull(cf, nullptr, 10) : (sphere_kernel ? 0u : pad);
+    kp.claim_fine = (uint32_t)(pad > fine ? pad - fine : 0);
     kp.out = (float4*)d_rgba;
     kp.counter = (uint32_t*)scratch;
     kp.stats = (unsigned long long*)((uint8_t*)scratch + 8);

@@ -70,6 +70,7 @@ void render_basic_kernel(KParams P) {
   bool walking = false; /* a segment is in flight (walk running, or finished and waiting to shade) */
   bool setup = false;   /* the lane's next segment needs its ray set up (a new sample, or a scattered ray) */
   Item it{0u, 0u, 0u, 0u};
+  WaveBlock wb{0u, 0u};
   Vec3 sum = v3(0.0f, 0.0f, 0.0f);
   PathState ps;
   init_path_state(ps);
@@ -97,7 +98,7 @@ void render_basic_kernel(KParams P) {
   for (;;) {
     /* lanes without work claim it; lanes with work but no segment in flight start a sample */
     const bool had_item = has_item;
-    claim_work(P, lane, has_item, exhausted, it);
+    claim_work(P, lane, has_item, exhausted, it, wb);
     if (has_item && !had_item) *slot_lds = it.slot;
     if (!__any(has_item || !exhausted)) break;
     if (has_item && !walking) {
