@@ -72,7 +72,7 @@ struct KParams {
   uint32_t walk_cap;   /* watchdog: more consecutive walk-loop iterations than any valid walk needs */
   uint32_t motion_uniform; /* every moving sphere has time0 = motion_t0, time1 - time0 = motion_span */
   float motion_t0, motion_span;
-  float4* partial; /* [n_chunks][n_out] chunk sums (n_chunks > 1) */
+  float4* partial; /* [n_out][n_chunks] chunk sums (n_chunks > 1): a pixel's chunks share cache lines */
   /* sphere-scene walk stream (layout.h; render_basic_kernel under CULL_EXACT) */
   const uint8_t* walk;
   uint32_t walk_bytes; /* whole stream */

@@ -240,10 +240,10 @@ __global__ __launch_bounds__(256) void reduce_chunks(const float4* __restrict__ 
                                                      uint32_t n_out, uint32_t n_chunks, uint32_t spp) {
   const float scale = 1.0f / (float)spp;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_out; i += gridDim.x * blockDim.x) {
-    float4 a = partial[i];
+    float4 a = partial[(size_t)i * n_chunks];
     Vec3 sum = v3(a.x, a.y, a.z);
     for (uint32_t c = 1; c < n_chunks; c++) {
-      float4 b = partial[(size_t)c * n_out + i];
+      float4 b = partial[(size_t)i * n_chunks + c];
       sum = sum + v3(b.x, b.y, b.z);
     }
     out[i] = make_float4(sqrtf(sum.x * scale), sqrtf(sum.y * scale), sqrtf(sum.z * scale), 1.0f);
@@ -640,14 +640,19 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
       throw HipError{HRT_ERR_INVALID_ARG, "hrt_render_tiles_device: null argument"};
     if (!s->committed || !s->d_blob) throw HipError{HRT_ERR_STATE, "scene not committed"};
     check_render_args(cam, p);
-    /* sample chunks: spp <= 64 keeps one work item per pixel (the reference's sequential sum);
-     * larger spp splits into <= 8 chunks of >= 64 samples so the frame's tail is a chunk, not a whole
-     * pixel.  Each chunk end costs a claim, a sample restart and a partial-sum store: 64 beats 32 by 10%
-     * on C2 (500 spp), 125 beats 63 by 1.6% on C3 */
+    /* sample chunks: spp <= 16 keeps one work item per pixel (the reference's sequential sum); larger
+     * spp splits into at most 32 chunks of >= 16 samples.  The chunks bound the frame's tail: the last
+     * items of a launch run alone, and a pixel whose paths bounce 50 times makes a long item (a 1/8-
+     * frame share of C2: chunks of 8 / 16 / 24 / 32 / 63 samples gave 12590 / 12330 / 11628 / 10796 /
+     * 9270 Mrays/s; the whole frame 14243 / 14489 / 14489 / 14338 / 13930).
+     * The rule is a function of spp alone, so every tile split sums a pixel's samples in the same
+     * chunks. */
     const uint32_t spp = p->samples;
-    const char* cm = getenv("HRT_CHUNK_MIN"); /* A/B knob: the smallest chunk (default 64) */
-    const uint32_t cmin = cm && atoi(cm) > 0 ? (uint32_t)atoi(cm) : 64u;
-    const uint32_t chunk = spp <= cmin ? spp : std::max<uint32_t>(cmin, (spp + 7) / 8);
+    const char* cm = getenv("HRT_CHUNK_MIN"); /* A/B knob: the smallest chunk (default 16) */
+    const uint32_t cmin = cm && atoi(cm) > 0 ? (uint32_t)atoi(cm) : 16u;
+    const char* cd = getenv("HRT_CHUNK_DIV"); /* A/B knob: at most this many chunks (default 32) */
+    const uint32_t cdiv = cd && atoi(cd) > 0 ? (uint32_t)atoi(cd) : 32u;
+    const uint32_t chunk = spp <= cmin ? spp : std::max<uint32_t>(cmin, (spp + cdiv - 1) / cdiv);
     const uint32_t n_chunks = (spp + chunk - 1) / chunk;
     std::vector<G::TileDev> td(n_tiles);
     uint64_t pad = 0, outp = 0;
@@ -660,7 +665,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
       pad += (uint64_t)bw * bh * 64 * n_chunks;
       outp += (uint64_t)t.w * t.h;
     }
-    /* work items and Item.slot (chunk x n_out + pixel <= pad) are 32-bit */
+    /* work items and Item.slot (pixel x n_chunks + chunk < pad) are 32-bit */
     /* headroom: waves claim blocks of CLAIM_BLOCK items past the end before they retire */
     if (pad >= 0xF0000000ull) throw HipError{HRT_ERR_UNSUPPORTED, "more than 3.75G pixel x sample-chunk items in one call"};
     hipStream_t stream = (hipStream_t)stream_;

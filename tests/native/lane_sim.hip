@@ -26,7 +26,7 @@ template <int CULL, int KIND>
 void render_pixel(const KParams& P, uint32_t px, uint32_t py, float* rgba, uint64_t* cnt) {
   constexpr bool FULL = KIND == 1;
   const uint32_t spp = P.spp;
-  const uint32_t chunk = spp <= 64 ? spp : std::max<uint32_t>(64, (spp + 7) / 8); /* render.hip */
+  const uint32_t chunk = spp <= 16 ? spp : std::max<uint32_t>(16, (spp + 31) / 32); /* render.hip */
   const uint32_t n_chunks = (spp + chunk - 1) / chunk;
   const float inf = u2f(0x7f800000u);
   Counts cn{0u, 0u, 0u, 0u, 0u, 0u};

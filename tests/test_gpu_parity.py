@@ -13,7 +13,7 @@ from oracle import oracle as O
 
 TOL = 1e-3
 
-# (preset, width, height, spp, depth): every scene feature of the reference; spp > 64 exercises the
+# (preset, width, height, spp, depth): every scene feature of the reference; spp > 16 exercises the
 # sample-chunk split (chunk sums reduced in a fixed order)
 CASES = [
     ("random", 40, 24, 100, 50),

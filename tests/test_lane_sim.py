@@ -64,7 +64,7 @@ def oracle_render(name, w, h, spp, depth, seed, earth, region=None, sample_offse
 
 CASES = [
     ("random", 40, 24, 8, 50),
-    ("random", 16, 12, 80, 50),          # two sample chunks
+    ("random", 24, 16, 40, 50),          # three sample chunks
     ("two_spheres", 48, 27, 8, 50),
     ("two_perlin_spheres", 48, 27, 8, 50),
     ("earth", 48, 27, 8, 50),
@@ -147,7 +147,7 @@ def test_depth_caps(sim, earth, depth):
 
 
 def test_headline_frame_band_at_500_spp(sim, earth):
-    """Two rows through the middle of the BASELINE frame (1920x1080, 500 spp, depth 50: 8 sample
+    """Two rows through the middle of the BASELINE frame (1920x1080, 500 spp, depth 50: 32 sample
     chunks) on the sphere kernel's lane, against the oracle."""
     region = (0, 539, 1920, 2)
     img, st = sim_render(sim, "random", 1920, 1080, 500, 50, 1, earth, kernel=0, cull=CULL_EXACT, region=region)
