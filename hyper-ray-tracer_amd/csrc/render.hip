@@ -640,19 +640,18 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
       throw HipError{HRT_ERR_INVALID_ARG, "hrt_render_tiles_device: null argument"};
     if (!s->committed || !s->d_blob) throw HipError{HRT_ERR_STATE, "scene not committed"};
     check_render_args(cam, p);
-    /* sample chunks: spp <= 16 keeps one work item per pixel (the reference's sequential sum); larger
-     * spp splits into at most 32 chunks of >= 16 samples.  The chunks bound the frame's tail: the last
-     * items of a launch run alone, and a pixel whose paths bounce 50 times makes a long item (a 1/8-
-     * frame share of C2: chunks of 8 / 16 / 24 / 32 / 63 samples gave 12590 / 12330 / 11628 / 10796 /
-     * 9270 Mrays/s; the whole frame 14243 / 14489 / 14489 / 14338 / 13930).
-     * The rule is a function of spp alone, so every tile split sums a pixel's samples in the same
-     * chunks. */
+    /* sample chunks (lane.h sample_chunk): they bound the frame's tail: the last items of a launch run
+     * alone, and a pixel whose paths bounce 50 times makes a long item (a 1/8-frame share of C2: chunks
+     * of 8 / 16 / 24 / 32 / 63 samples gave 12590 / 12330 / 11628 / 10796 / 9270 Mrays/s; the whole
+     * frame 14243 / 14489 / 14489 / 14338 / 13930).  The rule depends on spp and
+     * the scene's feature class only, so every tile split sums a pixel's samples in the same chunks. */
     const uint32_t spp = p->samples;
-    const char* cm = getenv("HRT_CHUNK_MIN"); /* A/B knob: the smallest chunk (default 16) */
-    const uint32_t cmin = cm && atoi(cm) > 0 ? (uint32_t)atoi(cm) : 16u;
-    const char* cd = getenv("HRT_CHUNK_DIV"); /* A/B knob: at most this many chunks (default 32) */
-    const uint32_t cdiv = cd && atoi(cd) > 0 ? (uint32_t)atoi(cd) : 32u;
-    const uint32_t chunk = spp <= cmin ? spp : std::max<uint32_t>(cmin, (spp + cdiv - 1) / cdiv);
+    const char* cm = getenv("HRT_CHUNK_MIN"); /* A/B knob: the smallest chunk (default 16 / 64) */
+    const uint32_t cmin = cm && atoi(cm) > 0 ? (uint32_t)atoi(cm) : 0u;
+    const char* cd = getenv("HRT_CHUNK_DIV"); /* A/B knob: at most this many chunks (default 32 / 8) */
+    const uint32_t cdiv = cd && atoi(cd) > 0 ? (uint32_t)atoi(cd) : 0u;
+    const bool general_scene = (s->feature_mask & ~G::F_BASIC) != 0;
+    const uint32_t chunk = sample_chunk(spp, general_scene, cmin, cdiv);
     const uint32_t n_chunks = (spp + chunk - 1) / chunk;
     std::vector<G::TileDev> td(n_tiles);
     uint64_t pad = 0, outp = 0;

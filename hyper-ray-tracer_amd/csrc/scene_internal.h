@@ -139,7 +139,7 @@ struct hrt_scene {
     void* h_tiles = nullptr;
     size_t tiles_cap = 0;
     void* event = nullptr; /* hipEvent_t */
-    void* d_partial = nullptr; /* sample-chunk sums [n_chunks][pixels] */
+    void* d_partial = nullptr; /* sample-chunk sums [pixels][n_chunks] */
     size_t partial_cap = 0;
     bool used = false;
   };

@@ -26,7 +26,7 @@ template <int CULL, int KIND>
 void render_pixel(const KParams& P, uint32_t px, uint32_t py, float* rgba, uint64_t* cnt) {
   constexpr bool FULL = KIND == 1;
   const uint32_t spp = P.spp;
-  const uint32_t chunk = spp <= 16 ? spp : std::max<uint32_t>(16, (spp + 31) / 32); /* render.hip */
+  const uint32_t chunk = P.chunk; /* render.hip: lane.h sample_chunk, set by the caller */
   const uint32_t n_chunks = (spp + chunk - 1) / chunk;
   const float inf = u2f(0x7f800000u);
   Counts cn{0u, 0u, 0u, 0u, 0u, 0u};
@@ -148,6 +148,7 @@ int lane_sim_render(const void* blob, const hrt_blob_info* bi, const hrt_camera*
   P.H = p->height;
   set_pixel_rcp(P);
   P.spp = p->samples;
+  P.chunk = sample_chunk(P.spp, (bi->feature_mask & ~G::F_BASIC) != 0);
   P.max_depth = p->max_depth;
   P.sample_offset = p->sample_offset;
   P.t_min = p->t_min;
