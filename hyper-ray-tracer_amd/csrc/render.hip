@@ -477,10 +477,12 @@ KParams scene_params(const hrt_scene* s, const hrt_camera* cam, const hrt_render
   kp.n_prims = (uint32_t)(pl.fast ? s->f_prims.size() : s->g_prims.size());
   kp.stream_len = pl.fast ? s->f_stream_len : 0;
   /* the sphere kernel's speculative walk (render_sphere.hip SPEC) blocks lanes less often: it runs best
-   * with smaller batches (sweep on C2) */
+   * with smaller batches; deep streams (top levels in LDS, w_hot: long walks) shade earlier (r02z sweep
+   * of postpone {40..56} x batch {4, 6, 8}: C2 best at 52-56 / 4, random-10k at 44 / 4, +1.8% over 48 / 6;
+   * DESIGN.md section 10) */
   const bool spec = !pl.full && !pl.general && !pl.fast && pl.cull == G::CULL_EXACT;
-  kp.postpone = env_knob("HRT_POSTPONE", spec ? 48 : 56);
-  kp.prim_batch = env_knob("HRT_PRIM_BATCH", spec ? 6 : 8);
+  kp.postpone = env_knob("HRT_POSTPONE", spec ? (s->w_hot ? 44 : 52) : 56);
+  kp.prim_batch = env_knob("HRT_PRIM_BATCH", spec ? 4 : 8);
   /* a walk visits each node at most once, a medium's boundary subtree at most twice per medium node */
   kp.walk_cap = 3u * (uint32_t)s->g_nodes.size() + 64u;
   kp.motion_uniform = s->motion_uniform ? 1u : 0u;
