@@ -82,15 +82,24 @@ struct KParams {
 };
 
 /* Sample-chunk size: spp <= cmin keeps one work item per pixel (the reference's sequential sum), larger
- * spp splits into at most cdiv chunks of >= cmin samples.  The defaults are a function of spp and of the
- * scene's feature class alone (never of the tile split), so every split sums a pixel's samples in the
- * same chunks.  Sphere scenes (render_basic_kernel: short passes, the launch tail dominates): >= 16
- * samples, <= 32 chunks.  General scenes (segment kernels: long iterations, per-lane claims, partial
- * writes that compete with the walks for memory): >= 64 samples, <= 8 chunks (C3 Earth+Perlin at
- * 1000 spp: 11483 Mrays/s with 8 chunks, 9703 with 32). */
-inline uint32_t sample_chunk(uint32_t spp, bool general_scene, uint32_t cmin = 0, uint32_t cdiv = 0) {
-  if (cmin == 0) cmin = general_scene ? 64u : 16u;
-  if (cdiv == 0) cdiv = general_scene ? 8u : 32u;
+ * spp splits into at most cdiv chunks of >= cmin samples.  The defaults depend on spp and on the scene's
+ * class alone (never on the tile split), so every split sums a pixel's samples in the same chunks.  A
+ * chunk should be long enough that claiming it and writing its partial sum are cheap next to its
+ * samples, and short enough that the launch's last items (run with the device mostly idle) end soon:
+ * - sphere scenes (render_basic_kernel: block claims, short passes): >= 16 samples, <= 32 chunks;
+ * - general scenes (segment kernels: per-lane claims): <= 8 chunks of >= 32 samples, or of >= 16 when
+ *   the main node stream is deep (> 1024 nodes: expensive samples, the tail dominates).
+ * Measured: Earth+Perlin 1000 spp 11447 Mrays/s with 8 chunks vs 9703 with 32;
+ * at 128 spp min 64 / 32 / 16 = 8934 / 9931 / 7930; Final 800^2 x 64 spp min 64 / 32 / 16 = 548 / 735 /
+ * 928; Cornell 64 spp 6900 / 6971 / 6963. */
+enum ChunkClass : uint32_t { CHUNK_SPHERE = 0, CHUNK_GENERAL = 1, CHUNK_GENERAL_DEEP = 2 };
+inline uint32_t chunk_class(uint32_t feature_mask, uint32_t main_nodes) {
+  if ((feature_mask & ~G::F_BASIC) == 0) return CHUNK_SPHERE;
+  return main_nodes > 1024u ? CHUNK_GENERAL_DEEP : CHUNK_GENERAL;
+}
+inline uint32_t sample_chunk(uint32_t spp, uint32_t cls, uint32_t cmin = 0, uint32_t cdiv = 0) {
+  if (cmin == 0) cmin = cls == CHUNK_GENERAL ? 32u : 16u;
+  if (cdiv == 0) cdiv = cls == CHUNK_SPHERE ? 32u : 8u;
   const uint32_t even = (spp + cdiv - 1) / cdiv;
   return spp <= cmin ? spp : (even > cmin ? even : cmin);
 }

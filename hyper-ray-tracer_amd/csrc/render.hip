@@ -648,12 +648,11 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
      * frame 14243 / 14489 / 14489 / 14338 / 13930).  The rule depends on spp and
      * the scene's feature class only, so every tile split sums a pixel's samples in the same chunks. */
     const uint32_t spp = p->samples;
-    const char* cm = getenv("HRT_CHUNK_MIN"); /* A/B knob: the smallest chunk (default 16 / 64) */
+    const char* cm = getenv("HRT_CHUNK_MIN"); /* A/B knob: the smallest chunk (default 16 / 32) */
     const uint32_t cmin = cm && atoi(cm) > 0 ? (uint32_t)atoi(cm) : 0u;
     const char* cd = getenv("HRT_CHUNK_DIV"); /* A/B knob: at most this many chunks (default 32 / 8) */
     const uint32_t cdiv = cd && atoi(cd) > 0 ? (uint32_t)atoi(cd) : 0u;
-    const bool general_scene = (s->feature_mask & ~G::F_BASIC) != 0;
-    const uint32_t chunk = sample_chunk(spp, general_scene, cmin, cdiv);
+    const uint32_t chunk = sample_chunk(spp, chunk_class(s->feature_mask, s->main_end), cmin, cdiv);
     const uint32_t n_chunks = (spp + chunk - 1) / chunk;
     std::vector<G::TileDev> td(n_tiles);
     uint64_t pad = 0, outp = 0;

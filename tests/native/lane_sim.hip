@@ -148,7 +148,7 @@ int lane_sim_render(const void* blob, const hrt_blob_info* bi, const hrt_camera*
   P.H = p->height;
   set_pixel_rcp(P);
   P.spp = p->samples;
-  P.chunk = sample_chunk(P.spp, (bi->feature_mask & ~G::F_BASIC) != 0);
+  P.chunk = sample_chunk(P.spp, chunk_class(bi->feature_mask, bi->main_end));
   P.max_depth = p->max_depth;
   P.sample_offset = p->sample_offset;
   P.t_min = p->t_min;

@@ -14,7 +14,7 @@ from oracle import oracle as O
 TOL = 1e-3
 
 # (preset, width, height, spp, depth): every scene feature of the reference; spp > 16 on sphere scenes
-# and spp > 64 on general ones exercises the sample-chunk split (chunk sums reduced in a fixed order)
+# and spp > 32 on general ones exercises the sample-chunk split (chunk sums reduced in a fixed order)
 CASES = [
     ("random", 40, 24, 100, 50),
     ("cornell", 24, 24, 70, 50),
