@@ -880,10 +880,12 @@ HRT_LANE_FI bool scatter(PathState& ps, const Rec& rec, uint32_t kind, Vec3 albe
   return false;
 }
 
+enum : int { TRIM_MEDIA = 1, TRIM_HEAVY_TEX = 2 };
+
 /* The part of one ray_color step after world.hit (application.rs:483-494): background on a miss,
  * else hit record, emission and scatter.  (ro, rd, rtime) is the segment just traced; the scattered
  * ray goes to ps.ro/ps.rd.  Returns true when the path is finished. */
-template <bool FULL, bool COUNT, bool LITE = false>
+template <bool FULL, bool COUNT, int TRIM = 0>
 HRT_LANE_FI bool shade(const KParams& P, PathState& ps, uint32_t winner, float closest, Vec3 ro,
                                       Vec3 rd, float rtime, float tau, Counts& cn) {
   if (winner == G::NONE) {
@@ -893,7 +895,7 @@ HRT_LANE_FI bool shade(const KParams& P, PathState& ps, uint32_t winner, float c
   const Rec rec = make_record<FULL>(P, winner, closest, ro, rd, rtime, tau);
   const G::Mat M = P.mats[rec.mat];
   return scatter<FULL>(ps, rec, M.kind, v3(M.a[0], M.a[1], M.a[2]), M.a[3], M.a[0], rd,
-                       [&]() { return tex_value<FULL && !LITE, COUNT>(P, M.tex, rec.u, rec.v, rec.p, cn); });
+                       [&]() { return tex_value<FULL && !(TRIM & TRIM_HEAVY_TEX), COUNT>(P, M.tex, rec.u, rec.v, rec.p, cn); });
 }
 
 /* shade() for the sphere kernel's walk stream: the winner is a leaf record (layout.h), which holds the
@@ -942,16 +944,17 @@ HRT_LANE_FI bool shade_walk(const KParams& P, const WalkSrc& src, PathState& ps,
 
 /* One step of ray_color (application.rs:477-495).  Returns true when the path is finished.
  * dbg (debug kernel only): receives o, d, time, t, winner of the traced segment.
- * LITE: a general scene without media, noise or image textures (Cornell): the medium branch of the walk
- * and the out-of-line texture call are compiled out (the scene has neither, so nothing changes). */
-template <int CULL, bool FULL, bool COUNT, bool FAST, bool LITE = false>
+ * TRIM (general scenes): features the scene does not have are compiled out, which changes nothing for
+ * it: TRIM_MEDIA the medium branch of the walk (no ConstantMedium), TRIM_HEAVY_TEX the out-of-line
+ * noise / image texture call (only solid and checker textures). */
+template <int CULL, bool FULL, bool COUNT, bool FAST, int TRIM = 0>
 HRT_LANE_FI bool segment(const KParams& P, const G::Node* nodes, const G::Prim* prims,
                                         PathState& ps, Counts& cn, float* dbg) {
   ps.traced = false;
   if (ps.depth_left == 0) return true; /* depth cap: black (:478-480) */
   float closest = u2f(0x7f800000u);
   uint32_t winner = G::NONE;
-  trace<CULL, FULL, FULL && !LITE, COUNT, FAST>(P, nodes, prims, 0u, P.main_end, ps.ro, ps.rd, ps.rtime, P.t_min, closest,
+  trace<CULL, FULL, FULL && !(TRIM & TRIM_MEDIA), COUNT, FAST>(P, nodes, prims, 0u, P.main_end, ps.ro, ps.rd, ps.rtime, P.t_min, closest,
                                        winner, ps.pk, cn);
   ps.traced = true;
   ps.pk.segment++;
@@ -961,7 +964,7 @@ HRT_LANE_FI bool segment(const KParams& P, const G::Node* nodes, const G::Prim* 
     dbg[6] = ps.rtime; dbg[7] = closest; dbg[8] = u2f(winner);
   }
   const float tau = P.motion_uniform ? (ps.rtime - P.motion_t0) / P.motion_span : 0.0f;
-  return shade<FULL, COUNT, LITE>(P, ps, winner, closest, ps.ro, ps.rd, ps.rtime, tau, cn);
+  return shade<FULL, COUNT, TRIM>(P, ps, winner, closest, ps.ro, ps.rd, ps.rtime, tau, cn);
 }
 
 HRT_LANE_FI void init_path_state(PathState& ps) {

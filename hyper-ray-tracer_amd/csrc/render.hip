@@ -77,7 +77,7 @@ constexpr int general_block_threads() { return FULL ? 256 : block_threads<LDS, F
 /* GW > 0: this instantiation is built for GW waves/SIMD (plan() picks 4 for general scenes: +18% on
  * Cornell, +4% on Final; 3, the compiler's choice, for small noise-texture scenes, whose Perlin path
  * spills at 128 VGPRs) */
-template <int CULL, bool FULL, bool COUNT, bool LDS, bool FAST, int GW = 0, bool LITE = false>
+template <int CULL, bool FULL, bool COUNT, bool LDS, bool FAST, int GW = 0, int TRIM = 0>
 __global__ __launch_bounds__((general_block_threads<FULL, LDS, FAST>()), (GW > 0 ? GW : general_min_waves<FULL, LDS, FAST>()))
 void render_kernel(KParams P) {
   extern __shared__ float4 lds_scene[];
@@ -111,7 +111,7 @@ void render_kernel(KParams P) {
       in_path = true;
     }
     const uint32_t nodes_before = cn.nodes;
-    const bool done = segment<CULL, FULL, COUNT, FAST, LITE>(P, nodes, prims, ps, cn, nullptr);
+    const bool done = segment<CULL, FULL, COUNT, FAST, TRIM>(P, nodes, prims, ps, cn, nullptr);
     if constexpr (COUNT) seg_nodes = cn.nodes - nodes_before;
     if (ps.traced) n_seg++;
     if (done) {
@@ -323,12 +323,12 @@ void take_slot_error(hrt_scene::Slot& sl) {
 }
 
 
-template <int CULL, bool FULL, bool COUNT, bool LDS, bool FAST, int GW = 0, bool LITE = false>
+template <int CULL, bool FULL, bool COUNT, bool LDS, bool FAST, int GW = 0, int TRIM = 0>
 void launch(const KParams& kp, int device, hipStream_t stream, size_t smem) {
-  const void* fn = (const void*)render_kernel<CULL, FULL, COUNT, LDS, FAST, GW, LITE>;
+  const void* fn = (const void*)render_kernel<CULL, FULL, COUNT, LDS, FAST, GW, TRIM>;
   const int block = general_block_threads<FULL, LDS, FAST>();
   const int grid = resident_grid(fn, block, device, LDS ? smem : 0, LDS);
-  hipLaunchKernelGGL((render_kernel<CULL, FULL, COUNT, LDS, FAST, GW, LITE>), dim3(grid), dim3(block), LDS ? smem : 0,
+  hipLaunchKernelGGL((render_kernel<CULL, FULL, COUNT, LDS, FAST, GW, TRIM>), dim3(grid), dim3(block), LDS ? smem : 0,
                      stream, kp);
   hip_check(hipGetLastError(), "render_kernel launch");
 }
@@ -352,7 +352,7 @@ constexpr size_t LDS_GEN_MAX = 48 * 1024;
 struct Plan {
   bool full, fast, lds;
   int gen_waves; /* general scenes under CULL_EXACT: the render_kernel<FULL> instantiation (3 or 4 waves/SIMD) */
-  bool lite;     /* general scene without media, noise or image textures: render_kernel<..., LITE> */
+  int trim;      /* general scenes: features compiled out of render_kernel (lane.h TRIM_*) */
   bool general; /* sphere scene forced onto the general kernel (diagnostics: HRT_KERNEL=general) */
   int cull;
   size_t smem;
@@ -388,9 +388,14 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
   if (pl.general && pl.full && (pl.smem > LDS_GEN_MAX || (gl && strcmp(gl, "0") == 0))) pl.lds = false;
   const char* gw = getenv("HRT_GEN_WAVES_RT"); /* A/B override: 3 or 4 */
   pl.gen_waves = gw ? (strcmp(gw, "3") == 0 ? 3 : 4) : ((s->feature_mask & G::F_NOISE) && pl.lds ? 3 : 4);
-  const char* lt = getenv("HRT_GEN_LITE"); /* A/B knob: "0" keeps the all-feature instantiation */
-  pl.lite = (s->feature_mask & (G::F_MEDIUM | G::F_NOISE | G::F_IMAGE)) == 0 && !s->media_nested &&
-            !(lt && strcmp(lt, "0") == 0);
+  const char* lt = getenv("HRT_GEN_TRIM"); /* A/B knob: "0" keeps the all-feature instantiation */
+  /* instantiated: all features (0), no noise / image textures (HEAVY_TEX: Cornell-smoke 124 VGPRs, no
+   * spills, +1.9%), neither those nor media (Cornell: 92 VGPRs, 5 waves/SIMD, +19%).  Trimming the
+   * medium branch alone measured -0.6 / -1% (Earth+Perlin, simple-light), so it is not built. */
+  pl.trim = 0;
+  if ((s->feature_mask & (G::F_NOISE | G::F_IMAGE)) == 0)
+    pl.trim = TRIM_HEAVY_TEX | ((s->feature_mask & G::F_MEDIUM) == 0 && !s->media_nested ? TRIM_MEDIA : 0);
+  if (lt && strcmp(lt, "0") == 0) pl.trim = 0;
   return pl;
 }
 
@@ -403,10 +408,14 @@ void launch_any(const hrt_scene* s, const Plan& pl, const KParams& kp, hipStream
   } else if (pl.general) {
     const int c = pl.cull;
     if (pl.full) {
-      if (c == G::CULL_EXACT && pl.gen_waves == 4 && pl.lite)
-        pl.lds ? launch<G::CULL_EXACT, true, COUNT, true, false, 4, true>(kp, s->device, stream, smem)
-               : launch<G::CULL_EXACT, true, COUNT, false, false, 4, true>(kp, s->device, stream, 0);
-      else if (c == G::CULL_EXACT && pl.gen_waves == 4)
+      if (c == G::CULL_EXACT && pl.gen_waves == 4 && pl.trim != 0) {
+        if (pl.trim == (TRIM_MEDIA | TRIM_HEAVY_TEX))
+          pl.lds ? launch<G::CULL_EXACT, true, COUNT, true, false, 4, TRIM_MEDIA | TRIM_HEAVY_TEX>(kp, s->device, stream, smem)
+                 : launch<G::CULL_EXACT, true, COUNT, false, false, 4, TRIM_MEDIA | TRIM_HEAVY_TEX>(kp, s->device, stream, 0);
+        else
+          pl.lds ? launch<G::CULL_EXACT, true, COUNT, true, false, 4, TRIM_HEAVY_TEX>(kp, s->device, stream, smem)
+                 : launch<G::CULL_EXACT, true, COUNT, false, false, 4, TRIM_HEAVY_TEX>(kp, s->device, stream, 0);
+      } else if (c == G::CULL_EXACT && pl.gen_waves == 4)
         pl.lds ? launch<G::CULL_EXACT, true, COUNT, true, false, 4>(kp, s->device, stream, smem)
                : launch<G::CULL_EXACT, true, COUNT, false, false, 4>(kp, s->device, stream, 0);
       else if (c == G::CULL_EXACT) pl.lds ? launch<G::CULL_EXACT, true, COUNT, true, false>(kp, s->device, stream, smem)
