@@ -117,11 +117,17 @@ __device__ __forceinline__ void claim_work(const KParams& P, uint32_t lane, bool
     exhausted = true;
     return;
   }
-  /* tile (binary search on pad_start), then [8x8 block][chunk][64 pixels] inside it */
-  uint32_t lo = 0, hi = P.n_tiles - 1;
-  while (lo < hi) {
-    uint32_t mid = (lo + hi + 1) >> 1;
-    if (P.tiles[mid].pad_start <= w) lo = mid; else hi = mid - 1;
+  /* tile (tiles padded to one stride: a division; else a binary search on pad_start), then [8x8 block]
+   * [chunk][64 pixels] inside it */
+  uint32_t lo = 0;
+  if (P.tile_stride) {
+    lo = w / P.tile_stride;
+  } else {
+    uint32_t hi = P.n_tiles - 1;
+    while (lo < hi) {
+      uint32_t mid = (lo + hi + 1) >> 1;
+      if (P.tiles[mid].pad_start <= w) lo = mid; else hi = mid - 1;
+    }
   }
   const G::TileDev T = P.tiles[lo];
   const uint32_t q = w - T.pad_start;

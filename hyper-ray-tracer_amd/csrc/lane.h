@@ -58,6 +58,7 @@ struct KParams {
   const G::TileDev* tiles;
   uint32_t n_tiles;
   uint32_t total_work;
+  uint32_t tile_stride; /* > 0: every tile's items padded to this many (tile = item / stride) */
   float4* out;
   uint32_t* counter;
   uint32_t claim_fine; /* work items from here on are claimed one per lane (kernel_common.h claim_work) */

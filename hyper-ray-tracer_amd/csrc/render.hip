@@ -681,6 +681,21 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
       pad += (uint64_t)bw * bh * 64 * n_chunks;
       outp += (uint64_t)t.w * t.h;
     }
+    /* Many tiles (a rank's share of the 16-px grid: 4080 tiles at 2 GPUs): a claim's binary search over
+     * the tile table was a dozen dependent global loads.  When padding every tile to the largest one's
+     * item count costs at most 1/8 more (idle) items, tile = item / stride instead (share of 2 / 8 on C2:
+     * DESIGN.md section 6.1). */
+    uint32_t stride = 0;
+    if (n_tiles > 1) {
+      uint64_t mx = 0;
+      for (uint32_t i = 0; i < n_tiles; i++) mx = std::max<uint64_t>(mx, (uint64_t)((td[i].w + 7) / 8) * ((td[i].h + 7) / 8) * 64 * n_chunks);
+      const char* ts = getenv("HRT_TILE_STRIDE"); /* A/B knob: "0" keeps the binary search */
+      if (mx * n_tiles <= pad + pad / 8 && mx * n_tiles < 0xF0000000ull && !(ts && strcmp(ts, "0") == 0)) {
+        stride = (uint32_t)mx;
+        for (uint32_t i = 0; i < n_tiles; i++) td[i].pad_start = i * stride;
+        pad = mx * n_tiles;
+      }
+    }
     /* work items and Item.slot (pixel x n_chunks + chunk < pad) are 32-bit */
     /* headroom: waves claim blocks of CLAIM_BLOCK items past the end before they retire */
     if (pad >= 0xF0000000ull) throw HipError{HRT_ERR_UNSUPPORTED, "more than 3.75G pixel x sample-chunk items in one call"};
@@ -698,24 +713,33 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
       take_slot_error(sl);
     }
     size_t tiles_bytes = n_tiles * sizeof(G::TileDev);
-    if (tiles_bytes > sl.tiles_cap) {
-      if (sl.d_mem) hip_check(hipFree(sl.d_mem), "hipFree(slot)");
-      if (sl.h_tiles) hip_check(hipHostFree(sl.h_tiles), "hipHostFree(slot)");
-      sl.d_mem = sl.h_tiles = nullptr;
-      sl.tiles_cap = 0;
-      size_t cap = std::max<size_t>(tiles_bytes, 64 * sizeof(G::TileDev));
-      hip_check(hipMalloc(&sl.d_mem, SLOT_HDR + cap), "hipMalloc(slot)");
-      hip_check(hipHostMalloc(&sl.h_tiles, SLOT_HDR + cap, hipHostMallocDefault), "hipHostMalloc(slot)");
-      sl.tiles_cap = cap;
-    }
     const size_t partial_bytes = n_chunks > 1 ? (size_t)n_chunks * outp * sizeof(float4) : 0;
-    if (partial_bytes > sl.partial_cap) {
-      if (sl.d_partial) hip_check(hipFree(sl.d_partial), "hipFree(partial)");
-      sl.d_partial = nullptr;
-      sl.partial_cap = 0;
-      hip_check(hipMalloc(&sl.d_partial, partial_bytes), "hipMalloc(partial)");
-      sl.partial_cap = partial_bytes;
-    }
+    auto grow = [&](hrt_scene::Slot& g) {
+      if (tiles_bytes > g.tiles_cap) {
+        if (g.d_mem) hip_check(hipFree(g.d_mem), "hipFree(slot)");
+        if (g.h_tiles) hip_check(hipHostFree(g.h_tiles), "hipHostFree(slot)");
+        g.d_mem = g.h_tiles = nullptr;
+        g.tiles_cap = 0;
+        size_t cap = std::max<size_t>(tiles_bytes, 64 * sizeof(G::TileDev));
+        hip_check(hipMalloc(&g.d_mem, SLOT_HDR + cap), "hipMalloc(slot)");
+        hip_check(hipHostMalloc(&g.h_tiles, SLOT_HDR + cap, hipHostMallocDefault), "hipHostMalloc(slot)");
+        g.tiles_cap = cap;
+      }
+      if (partial_bytes > g.partial_cap) {
+        if (g.d_partial) hip_check(hipFree(g.d_partial), "hipFree(partial)");
+        g.d_partial = nullptr;
+        g.partial_cap = 0;
+        hip_check(hipMalloc(&g.d_partial, partial_bytes), "hipMalloc(partial)");
+        g.partial_cap = partial_bytes;
+      }
+    };
+    /* slots never launched are grown with this one, so the next calls (e.g. a timed loop that keeps
+     * several launches in flight) do not allocate pinned and device memory between launches */
+    const bool first_growth = tiles_bytes > sl.tiles_cap || partial_bytes > sl.partial_cap;
+    grow(sl);
+    if (first_growth)
+      for (auto& other : s->slots)
+        if (&other != &sl && !other.used) grow(other);
     void* scratch = sl.d_mem;
     memcpy((uint8_t*)sl.h_tiles + SLOT_HDR, td.data(), tiles_bytes);
     hip_check(hipMemsetAsync(scratch, 0, SLOT_HDR, stream), "hipMemsetAsync");
@@ -726,6 +750,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     kp.tiles = (const G::TileDev*)((uint8_t*)scratch + SLOT_HDR);
     kp.n_tiles = n_tiles;
     kp.total_work = (uint32_t)pad;
+    kp.tile_stride = stride;
     /* the sphere kernel claims blocks of items to the end: its passes are short, and per-lane claims
      * made them wait on the contended counter (r02y: +12% on C2; per-lane claims for the last 0.26 /
      * 1 / 4 M items measured +0.7 / -0.5 / -3% on C2 and -1 / -9 / -6% on a 1/8-frame share).  The

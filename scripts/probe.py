@@ -20,6 +20,7 @@ ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--ab", default="", help="comma list of flag values to alternate (A/B in one process)")
 ap.add_argument("--env", default="", help="/-list of NAME=VALUE[,NAME=VALUE] env settings to alternate (A/B)")
 ap.add_argument("--count", action="store_true", help="also run one instrumented pass per variant")
+ap.add_argument("--share", type=int, default=1, help="render rank 0's share of an N-way tile split (hrt/tiling.py)")
 a = ap.parse_args()
 
 _earth = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden", "earthmap_rgb8.png")
@@ -44,6 +45,10 @@ def clear_env(e):
         os.environ.pop(kv.split("=", 1)[0], None)
 out = torch.empty((a.height, a.width, 4), dtype=torch.float32, device="cuda")
 tiles = [(0, 0, a.width, a.height)]
+if a.share > 1:
+    from hrt import tiling
+    tiles = [tuple(t) for t in tiling.split_tiles(a.width, a.height, a.share, 0)]
+    print(f"share 0 of {a.share}: {len(tiles)} tiles, {tiling.share_pixels(tiles)} pixels", flush=True)
 res = {k: [] for k in flag_sets}
 imgs = {}
 for r in range(a.reps):
