@@ -119,3 +119,49 @@ def test_bvh_tie_order_sensitivity(name, W, H, spp, earth, monkeypatch):
           f"max {diff.max():.3g}")
     assert ta > 0
     assert (diff > 1e-3).mean() < 1e-3  # at most 0.1% of the pixels change beyond the parity bar
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,tile", [(3, 16), (8, 16), (2, 40)])
+def test_tile_stride_lookup_equals_binary_search(world, tile, earth, monkeypatch):
+    """A share's tiles padded to one stride (tile = item / stride, render.hip) against the binary search
+    over the tile table (HRT_TILE_STRIDE=0): same work items, so the same bits and ray counts; ragged
+    tiles (320 x 180 with 16- and 40-px tiles) pad to the largest tile."""
+    import torch
+
+    from hrt import tiling
+
+    W, H = 320, 180
+    s = hrt.preset("random", 1, earth)
+    s.commit()
+    cam = hrt.preset_camera(s.info, W, H)
+    p = hrt.params(W, H, 40, 50, 5, tuple(s.info.background))
+    t = tiling.split_tiles(W, H, world, world - 1, tile)
+    out = []
+    for knob in (None, "0"):
+        if knob is None:
+            monkeypatch.delenv("HRT_TILE_STRIDE", raising=False)
+        else:
+            monkeypatch.setenv("HRT_TILE_STRIDE", knob)
+        d = torch.empty(tiling.share_pixels(t) * 4, dtype=torch.float32, device="cuda")
+        st = hrt.render_tiles_device(s, cam, p, t, d.data_ptr(), 0, want_stats=True)
+        out.append((int(st.segments), int(st.pixels), d.cpu().numpy()))
+    assert out[0][0] == out[1][0] and out[0][1] == out[1][1] == tiling.share_pixels(t)
+    assert np.array_equal(out[0][2], out[1][2])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,w,h,spp", [("cornell", 64, 64, 40), ("cornell_smoke", 48, 48, 40)])
+def test_trimmed_general_kernel_equals_all_feature_kernel(name, w, h, spp, earth, monkeypatch):
+    """render_kernel<..., TRIM> (features the scene lacks compiled out: Cornell no media and no heavy
+    textures, Cornell-smoke no heavy textures) against the all-feature instantiation (HRT_GEN_TRIM=0)."""
+    s = hrt.preset(name, 1, earth)
+    s.commit()
+    cam = hrt.preset_camera(s.info, w, h)
+    p = hrt.params(w, h, spp, 50, 9, tuple(s.info.background))
+    monkeypatch.delenv("HRT_GEN_TRIM", raising=False)
+    a, sa = hrt.render(s, cam, p, stats=True)
+    monkeypatch.setenv("HRT_GEN_TRIM", "0")
+    b, sb = hrt.render(s, cam, p, stats=True)
+    assert sa.segments == sb.segments
+    assert np.array_equal(a, b)
