@@ -364,7 +364,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 2),
             "higher_is_better": True,
-            "scaling": "strong" if world > 1 and tiled else "weak",
+            "scaling": "strong" if tiled else "weak",  # tiles: the frame is the fixed total at every N
             "vs_baseline": None,
             "dtype": "f32",
             "data": SCENE_DATA.get(args.preset, "synthetic (seeded scene builder)"),
