@@ -76,6 +76,8 @@ CASES = [
     ("random_10k", 32, 18, 2, 50),
     ("features", 48, 27, 8, 50),
     ("cornell", 24, 24, 4, 2),           # depth cap
+    ("cornell", 12, 12, 70, 50),         # general scene: three chunks of >= 32 samples (lane.h sample_chunk)
+    ("final", 8, 8, 40, 50),             # deep general scene (> 1024 nodes): three chunks of >= 16
 ]
 
 
