@@ -77,6 +77,10 @@ def parse():
     ap.add_argument("--save", default="", help="write rank 0's last timed frame here (.pfm exact / .ppm 8-bit)")
     ap.add_argument("--one-device", action="store_true",
                     help="every rank on GPU 0 (rehearsal of the N > 1 path on a one-GPU box; not a scaling figure)")
+    ap.add_argument("--share", type=int, default=1,
+                    help="one process: render rank 0's share of an N-way tile split (one GPU's part of an N-GPU frame)")
+    ap.add_argument("--no-delivery", action="store_true",
+                    help="skip the per-frame delivery phase (frame_ms: launch + D2H + host placement, pipelined)")
     return ap.parse_args()
 
 
@@ -181,7 +185,44 @@ def cpu_leg(args, frame_rays_per_sample):
     return cb, rows, img, c
 
 
-def roofline_obj(args, scene, cam, bg, tiles, p, out_ptr, stream, launch_ms, seg_step, n_px):
+def pmc_key(args, share):
+    """profiles/roofline_pmc.json key of the launch this run times: the preset, the frame and spp, and for a
+    tile split the share (rank 0's of `share` ranks), whose counters are those of that share's launch."""
+    return f"{args.preset}_{args.width}x{args.height}_{args.spp}" + (f"_share{share}" if share > 1 else "")
+
+
+def load_pmc(key):
+    try:
+        return json.load(open(os.path.join(ROOT, "profiles", "roofline_pmc.json"))).get(key)
+    except (OSError, ValueError):
+        return None
+
+
+def apply_pmc(ro, key, pm, launch_s, seg_step):
+    """Fill the roofline object's counter fields from the PMC record of this launch's workload (`key`);
+    counters that would put the launch above peak belong to another workload and are rejected."""
+    ro["pmc_key"] = key
+    if pm and pm.get("valu_insts"):
+        sha = hashlib.sha256(open(hrt.LIB_PATH, "rb").read()).hexdigest()[:16]
+        ach = pm["valu_insts"] / launch_s / 1e9
+        ro.update(achieved=round(ach, 1), frac=round(ach / ro["peak"], 4), traffic=pm.get("hbm_bytes"),
+                  pmc_source=pm["source"], pmc_build_match=(pm.get("lib_sha16") == sha), lib_sha16=sha,
+                  valu_insts_per_launch=pm["valu_insts"], valu_insts_per_ray=round(pm["valu_insts"] / max(1, seg_step), 2))
+        if pm.get("clock_hz"):
+            ro["clock_ghz_profiled"] = round(pm["clock_hz"] / 1e9, 3)
+            ro["frac_at_profiled_clock"] = round(pm["valu_insts"] * VALU_CYC / (SIMDS * pm["clock_hz"] * launch_s), 4)
+        if pm.get("hbm_bytes"):
+            ro["hbm_counter_GBs"] = round(pm["hbm_bytes"] / launch_s / 1e9, 2)
+            ro["hbm_frac"] = round(pm["hbm_bytes"] / launch_s / 1e9 / PEAK_HBM_GBS, 5)
+        if pm.get("sq_lds_idx_active"):
+            ro["lds_bank_conflict_share"] = round(pm["sq_lds_bank_conflict"] / pm["sq_lds_idx_active"], 4)
+        if ro["frac"] > 1.0:
+            # counters of another workload (or build) than this launch: never report above peak
+            ro.update(achieved=None, frac=None, frac_at_profiled_clock=None,
+                      pmc_rejected=f"counters of {key} give {ach:.0f} > peak over this launch's time")
+
+
+def roofline_obj(args, scene, cam, bg, tiles, p, out_ptr, stream, launch_ms, seg_step, n_px, share=1):
     """The kernel's bound and where it sits (rank 0, instrumented pass outside the timed region)."""
     pc = hrt.params(args.width, args.height, args.spp, args.depth, args.seed, bg, sample_offset=p.sample_offset,
                     flags=hrt.RENDER_COUNT_WORK)
@@ -203,27 +244,59 @@ def roofline_obj(args, scene, cam, bg, tiles, p, out_ptr, stream, launch_ms, seg
         "note": "achieved = SQ_INSTS_VALU of one launch of this build (rocprofv3 PMC, profiles/) / the live "
                 "HIP-event launch time; peak = 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction",
     }
-    pj = os.path.join(ROOT, "profiles", "roofline_pmc.json")
-    key = f"{args.preset}_{args.width}x{args.height}_{args.spp}"
-    try:
-        pm = json.load(open(pj)).get(key)
-    except (OSError, ValueError):
-        pm = None
-    if pm and pm.get("valu_insts"):
-        sha = hashlib.sha256(open(hrt.LIB_PATH, "rb").read()).hexdigest()[:16]
-        ach = pm["valu_insts"] / launch_s / 1e9
-        ro.update(achieved=round(ach, 1), frac=round(ach / ro["peak"], 4), traffic=pm.get("hbm_bytes"),
-                  pmc_source=pm["source"], pmc_build_match=(pm.get("lib_sha16") == sha), lib_sha16=sha,
-                  valu_insts_per_launch=pm["valu_insts"], valu_insts_per_ray=round(pm["valu_insts"] / max(1, seg_step), 2))
-        if pm.get("clock_hz"):
-            ro["clock_ghz_profiled"] = round(pm["clock_hz"] / 1e9, 3)
-            ro["frac_at_profiled_clock"] = round(pm["valu_insts"] * VALU_CYC / (SIMDS * pm["clock_hz"] * launch_s), 4)
-        if pm.get("hbm_bytes"):
-            ro["hbm_counter_GBs"] = round(pm["hbm_bytes"] / launch_s / 1e9, 2)
-            ro["hbm_frac"] = round(pm["hbm_bytes"] / launch_s / 1e9 / PEAK_HBM_GBS, 5)
-        if pm.get("sq_lds_idx_active"):
-            ro["lds_bank_conflict_share"] = round(pm["sq_lds_bank_conflict"] / pm["sq_lds_idx_active"], 4)
+    key = pmc_key(args, share)
+    apply_pmc(ro, key, load_pmc(key), launch_s, seg_step)
     return ro
+
+
+def delivery_phase(args, scene, cam, p, tiles, n_px, dev, stream, world, rank, barrier, W, H, ms_per_step):
+    """K more steps, each launch followed by its frame's delivery to the host (hrt/delivery.py): D2H copy
+    of the share into pinned memory on a second stream, placement into a node-wide shared-memory frame
+    by a worker thread, rank 0 handing the completed frame over; double-buffered, so frame k is copied
+    and placed while frame k + 1 renders.  Returns (delivery dict for rank 0's line, rank 0's last
+    delivered frame or None)."""
+    from hrt import delivery
+
+    outs = [torch.empty(n_px * 4, dtype=torch.float32, device=dev) for _ in range(2)]
+    K = args.steps
+    last = {}
+
+    def keep(k, f):
+        if k == K:  # the last timed frame (step 0 is the untimed warm-up through the pipeline)
+            last["frame"] = f.copy()
+
+    fd = delivery.FrameDelivery(W, H, world, rank, tiles, on_frame=keep, device=dev)
+    try:
+        for k in range(K + 1):
+            if k == 1:  # step 0 warmed the pipeline (pinned pages, placement index, shared frame)
+                fd.flush(1)
+                barrier()
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+            fd.before_launch(k, stream)
+            hrt.render_tiles_device(scene, cam, p, tiles, outs[k % 2].data_ptr(), stream.cuda_stream)
+            fd.submit(k, outs[k % 2], stream)
+        fd.flush(K + 1)
+        barrier()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            import torch.distributed as dist
+
+            t = torch.tensor([dt], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t[0])
+        scene.synchronize()
+    finally:
+        barrier()
+        fd.close()
+    frame_ms = dt / K * 1e3
+    d = {"frame_ms": round(frame_ms, 2), "ms_per_step": round(ms_per_step, 2),
+         "frame_vs_launch": round(frame_ms / max(1e-9, ms_per_step), 4), "frames": K,
+         "bytes_per_frame": W * H * 16,
+         "path": "each step: launch into one of two device buffers; D2H of the share into pinned memory on a copy "
+                 "stream; a worker thread per rank places it into a double-buffered frame in host shared memory; "
+                 "rank 0 hands over each completed frame (hrt/delivery.py)"}
+    return d, last.get("frame")
 
 
 def main():
@@ -247,7 +320,11 @@ def main():
     cam = hrt.preset_camera(scene.info, W, H)
     bg = tuple(scene.info.background)
     tiled = args.scaling == "tiles"
-    if world == 1:
+    share = world if (world > 1 and tiled) else max(1, args.share)
+    if world == 1 and share > 1:  # one GPU's part of a share-way frame (config lines of C4 / C5)
+        tiles = tiling.split_tiles(W, H, share, 0, args.tile)
+        p = hrt.params(W, H, args.spp, args.depth, args.seed, bg)
+    elif world == 1:
         tiles = [(0, 0, W, H)]  # the union of the grid: one launch over the frame
         p = hrt.params(W, H, args.spp, args.depth, args.seed, bg)
     elif tiled:
@@ -266,8 +343,10 @@ def main():
     seg_step, samples_step = int(st.segments), int(st.samples)
     warm_s = time.perf_counter() - tw
     progress = warm_s > 20.0  # long frames: a progress line per timed frame
-    log(f"warm-up frame: {seg_step} rays in {warm_s:.1f} s")
-    for _ in range(max(0, args.warmup - 1)):
+    log(f"work-count frame: {seg_step} rays in {warm_s:.1f} s")
+    # W warm-up steps as the timed ones run them (asynchronous launches: the first one also sizes the
+    # library's other in-flight slots, so no timed step allocates device or pinned memory)
+    for _ in range(max(1, args.warmup)):
         hrt.render_tiles_device(scene, cam, p, tiles, out.data_ptr(), stream.cuda_stream)
 
     def barrier():
@@ -306,17 +385,25 @@ def main():
         seg_all, samples_all = float(seg_step), float(samples_step)
     value = seg_all * args.steps / dt / 1e6
 
-    # N > 1, tile split: gather the shares to rank 0 (host, gloo) and check the frame bit for bit
+    # per-frame delivery (launch + D2H + placement into the host frame, pipelined): frame_ms beside the
+    # launch-only ms_per_step; for N > 1 the delivered frame is the host gather that the bit-identity
+    # check below uses
     frame_check = None
     frame = None
+    deliv = None
+    if not args.no_delivery and (world > 1 or share == 1):
+        deliv, frame = delivery_phase(args, scene, cam, p, tiles, n_px, dev, stream, world, rank, barrier, W, H,
+                                      ms_per_step=dt / args.steps * 1e3)
     if world > 1 and tiled:
         tg = time.perf_counter()
-        frame = tiling.gather_frame(out.cpu().numpy(), W, H, world, rank,
-                                    shares=lambda r: tiling.split_tiles(W, H, world, r, args.tile))
+        if frame is None:
+            frame = tiling.gather_frame(out.cpu().numpy(), W, H, world, rank,
+                                        shares=lambda r: tiling.split_tiles(W, H, world, r, args.tile))
         gather_s = time.perf_counter() - tg
         if rank == 0:
             frame_check = {"gathered_pixels": int((frame[..., 3] == 1.0).sum()), "frame_pixels": W * H,
-                           "gather_ms": round(gather_s * 1e3, 1), "tile": args.tile,
+                           "gather": "delivered frame (pipelined shared-memory gather)" if deliv else "gloo gather after the timed steps",
+                           "gather_ms": None if deliv else round(gather_s * 1e3, 1), "tile": args.tile,
                            "rank_launch_ms": rank_ms, "imbalance": round(max(rank_ms) / max(1e-9, min(rank_ms)), 4)}
             if not args.no_frame_check:
                 ref = torch.empty(W * H * 4, dtype=torch.float32, device=dev)
@@ -328,7 +415,7 @@ def main():
                 if not same:
                     raise SystemExit("gathered multi-GPU frame differs from the 1-GPU frame")
         barrier()
-    elif world == 1:
+    elif world == 1 and share == 1:
         frame = out.view(H, W, 4)
 
     cpu, parity = None, None
@@ -349,7 +436,8 @@ def main():
 
     roofline = None
     if rank == 0:
-        roofline = roofline_obj(args, scene, cam, bg, tiles, p, out.data_ptr(), stream.cuda_stream, launch_ms, seg_step, n_px)
+        roofline = roofline_obj(args, scene, cam, bg, tiles, p, out.data_ptr(), stream.cuda_stream, launch_ms, seg_step, n_px,
+                                share=share)
 
     if rank == 0 and args.save and frame is not None:
         hrt.write_image(args.save, frame.cpu().numpy() if torch.is_tensor(frame) else frame)
@@ -359,7 +447,7 @@ def main():
             "metric": "Mrays/sec at 1920x1080, 500 spp, RTIOW final scene; per-pixel Linf vs CPU ref",
             "value": round(value, 2),
             "unit": "Mrays/s",
-            "n_gpus": world,
+            "n_gpus": 1 if args.one_device else world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 2),
@@ -376,16 +464,23 @@ def main():
                 "msamples_per_s": round(samples_all * args.steps / dt / 1e6, 2),
                 "parallelism": (f"{world} GPU(s), frame tiled ({args.tile}-px tiles, diagonal interleave), host gather, no collectives"
                                 if world > 1 and tiled else f"{world} GPU(s), " + ("replicas" if world > 1 else "one launch per frame")),
+                **({"share": f"rank 0 of a {share}-way tile split ({args.tile}-px tiles): one GPU's part of a {share}-GPU frame",
+                    "share_pixels": n_px} if world == 1 and share > 1 else {}),
                 "cull_mode": {0: "reference", 1: "slab (approximate)", 2: "exact (reference test + provably safe culling)"}[si.cull_mode],
             },
             "parity": parity,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        if deliv is not None:
+            line["delivery"] = deliv
         if frame_check is not None:
             line["frame_check"] = frame_check
         if args.one_device and world > 1:
-            line["note"] = "--one-device: all ranks shared GPU 0 (a rehearsal of the multi-GPU path, not a scaling figure)"
+            line["ranks"] = world
+            line["rehearsal"] = True
+            line["note"] = (f"--one-device: all {world} ranks shared GPU 0 (a rehearsal of the multi-GPU path, not a "
+                            "scaling figure): n_gpus counts distinct devices")
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

@@ -265,6 +265,7 @@ extern "C" hrt_status hrt_preset_build(hrt_scene* s, int32_t preset, uint64_t sc
     switch (preset) {
       case HRT_PRESET_RANDOM: info->aperture = 0.1f; world = generate_random_scene(c, 11); break;
       case HRT_PRESET_RANDOM_10K: info->aperture = 0.1f; world = generate_random_scene(c, 50); break;
+      case HRT_PRESET_RANDOM_40K: info->aperture = 0.1f; world = generate_random_scene(c, 100); break;
       case HRT_PRESET_TWO_SPHERES: world = generate_two_spheres(); break;
       case HRT_PRESET_TWO_PERLIN_SPHERES: world = generate_two_perlin_spheres(c); break;
       case HRT_PRESET_EARTH: world = generate_earth(c); break;

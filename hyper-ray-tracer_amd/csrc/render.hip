@@ -714,7 +714,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     }
     size_t tiles_bytes = n_tiles * sizeof(G::TileDev);
     const size_t partial_bytes = n_chunks > 1 ? (size_t)n_chunks * outp * sizeof(float4) : 0;
-    auto grow = [&](hrt_scene::Slot& g) {
+    auto grow = [&](hrt_scene::Slot& g, bool partial) {
       if (tiles_bytes > g.tiles_cap) {
         if (g.d_mem) hip_check(hipFree(g.d_mem), "hipFree(slot)");
         if (g.h_tiles) hip_check(hipHostFree(g.h_tiles), "hipHostFree(slot)");
@@ -725,7 +725,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
         hip_check(hipHostMalloc(&g.h_tiles, SLOT_HDR + cap, hipHostMallocDefault), "hipHostMalloc(slot)");
         g.tiles_cap = cap;
       }
-      if (partial_bytes > g.partial_cap) {
+      if (partial && partial_bytes > g.partial_cap) {
         if (g.d_partial) hip_check(hipFree(g.d_partial), "hipFree(partial)");
         g.d_partial = nullptr;
         g.partial_cap = 0;
@@ -734,12 +734,15 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
       }
     };
     /* slots never launched are grown with this one, so the next calls (e.g. a timed loop that keeps
-     * several launches in flight) do not allocate pinned and device memory between launches */
+     * several launches in flight) do not allocate pinned and device memory between launches.  Their
+     * partial-sum buffers (a pixel's chunk sums: 1 GB for C2's 32 chunks) only when this call is
+     * asynchronous (no stats): a synchronous caller (hrt_render, a progressive batch with stats) never
+     * has a second launch in flight, and would otherwise hold N_SLOTS such buffers. */
     const bool first_growth = tiles_bytes > sl.tiles_cap || partial_bytes > sl.partial_cap;
-    grow(sl);
+    grow(sl, true);
     if (first_growth)
       for (auto& other : s->slots)
-        if (&other != &sl && !other.used) grow(other);
+        if (&other != &sl && !other.used) grow(other, stats == nullptr);
     void* scratch = sl.d_mem;
     memcpy((uint8_t*)sl.h_tiles + SLOT_HDR, td.data(), tiles_bytes);
     hip_check(hipMemsetAsync(scratch, 0, SLOT_HDR, stream), "hipMemsetAsync");

@@ -38,6 +38,7 @@ PRESETS = {
     "earth_perlin": 8,
     "random_10k": 9,
     "features": 10,
+    "random_40k": 11,  # build-defined: 39.9k leaves, the device-built walk hierarchy by default
 }
 
 

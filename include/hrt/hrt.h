@@ -146,7 +146,9 @@ enum {
   HRT_PRESET_EARTH_PERLIN = 8,       /* config 3: earth (0,2,0) r2 over the Perlin ground of :589-602 */
   HRT_PRESET_RANDOM_10K = 9,         /* config 4: :511-545 with a, b in [-50, 50) */
   HRT_PRESET_FEATURES = 10,          /* X/Z rotations, lists, nested instances, media in instances */
-  HRT_PRESET_COUNT = 11
+  HRT_PRESET_RANDOM_40K = 11,        /* :511-545 with a, b in [-100, 100): 39.9k leaves, so the walk stream's
+                                        hierarchy is built on the device by default */
+  HRT_PRESET_COUNT = 12
 };
 
 const char* hrt_last_error(void);

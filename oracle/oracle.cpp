@@ -895,6 +895,10 @@ static Scene* build_preset(int preset, uint64_t seed, const uint8_t* img, uint32
       I.aperture = 0.1f;
       sc->world = random_scene(B, 50);
       break;
+    case 11: /* 40k spheres (a device-built walk hierarchy in the library) */
+      I.aperture = 0.1f;
+      sc->world = random_scene(B, 100);
+      break;
     case 1: { /* TwoSpheres :567-587 */
       MatP checker = lambert(
           std::make_shared<CheckerTexture>(solid(0.2f, 0.3f, 0.1f), solid(0.9f, 0.9f, 0.9f)));

@@ -1,6 +1,6 @@
 """Summarise rocprofv3 outputs (kernel stats + FETCH/WRITE/SQ PMC passes) of one bench run.
 
-  python scripts/summarize_profile.py <tag> <preset> <W> <H> <spp>
+  python scripts/summarize_profile.py <tag> <preset> <W> <H> <spp> [share]
 Reads gpurun_out/prof_<tag>_{kt,fetch,write,sq,sq2}/ (scripts/profile.sh), writes
 profiles/<tag>_summary.md (+ the raw kernel_stats csv) and updates profiles/roofline_pmc.json, which
 bench.py reads for its `roofline` object:
@@ -29,6 +29,7 @@ def lib_sha16():
 
 def main():
     tag, preset, W, H, spp = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
+    share = int(sys.argv[6]) if len(sys.argv) > 6 and sys.argv[6].isdigit() else 1
     src = os.path.join(ROOT, "gpurun_out")
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
@@ -51,7 +52,8 @@ def main():
                 return name, v
         return None, {}
 
-    lines = [f"# rocprofv3 summary `{tag}`: bench.py, {preset} {W}x{H} {spp} spp\n"]
+    lines = [f"# rocprofv3 summary `{tag}`: bench.py, {preset} {W}x{H} {spp} spp"
+             + (f", rank 0's share of a {share}-way tile split" if share > 1 else "") + "\n"]
     kt = os.path.join(src, f"prof_{tag}_kt", "run_kernel_stats.csv")
     kern_ms = None
     kname = None
@@ -123,7 +125,7 @@ def main():
         fh.write("\n".join(lines) + "\n")
     pj = os.path.join(dst, "roofline_pmc.json")
     d = json.load(open(pj)) if os.path.exists(pj) else {}
-    d[f"{preset}_{W}x{H}_{spp}"] = res
+    d[f"{preset}_{W}x{H}_{spp}" + (f"_share{share}" if share > 1 else "")] = res
     with open(pj, "w") as fh:
         json.dump(d, fh, indent=1)
     print("\n".join(lines))

@@ -23,3 +23,22 @@ def test_band_rows_spread_over_the_frame():
     r = bench.band_rows(1080, 60)
     assert len(r) == 60 and r[0] < 18 and r[-1] > 1060
     assert bench.band_rows(10, 50) == list(range(10))
+
+
+def test_pmc_key_names_the_share_and_rejects_counters_above_peak():
+    """A tile split's launch is priced with the counters of that share's launch (key suffix _shareN), never
+    with the whole frame's; counters that would put a launch above peak are rejected, not reported."""
+    args = argparse.Namespace(preset="random", width=1920, height=1080, spp=500)
+    assert bench.pmc_key(args, 1) == "random_1920x1080_500"
+    assert bench.pmc_key(args, 8) == "random_1920x1080_500_share8"
+    peak = bench.SIMDS * bench.MAX_CLOCK_HZ / bench.VALU_CYC / 1e9
+    pm = {"valu_insts": 2.0e11, "source": "x", "lib_sha16": None}
+    ro = {"peak": peak, "achieved": None, "frac": None}
+    bench.apply_pmc(ro, "k", pm, 0.203, 2.9e9)
+    assert 0.7 < ro["frac"] < 0.9 and ro["pmc_key"] == "k"
+    ro = {"peak": peak, "achieved": None, "frac": None}
+    bench.apply_pmc(ro, "k", pm, 0.203 / 8, 2.9e9 / 8)  # a 1/8 share's launch with the whole frame's counters
+    assert ro["frac"] is None and ro["achieved"] is None and "pmc_rejected" in ro
+    ro = {"peak": peak, "achieved": None, "frac": None}
+    bench.apply_pmc(ro, "k", None, 0.2, 1e9)
+    assert ro["frac"] is None and ro["pmc_key"] == "k"

@@ -47,8 +47,10 @@ def test_c1_random_400x225_50spp_whole_frame(earth):
 BANDS = [
     ("random", 1920, 1080, 500, [37, 540, 1001], 0, None),           # C2 (also bench.py's parity band)
     ("earth_perlin", 1920, 1080, 1000, [100, 520, 700], 0, None),    # C3: image texture + Perlin ground
-    ("random_10k", 3840, 2160, 2000, [1080], 1856, 128),             # C4: 7 MB scene in global memory
-    ("cornell", 2048, 2048, 1250, [300, 1024, 1900], 0, None),       # C5: one GPU's share of 10000 spp
+    ("random_10k", 3840, 2160, 2000, [400], 1664, 512),   # C4: 1.6 MB walk stream, LDS + global memory;
+    ("random_10k", 3840, 2160, 2000, [1080], 1664, 512),  # three 512-px bands (the oracle's reference
+    ("random_10k", 3840, 2160, 2000, [1700], 1664, 512),  # culling runs ~0.3 Mrays/s here: ~10 s each)
+    ("cornell", 2048, 2048, 1250, [300, 1024, 1900], 0, None),       # C5 at 1250 spp (one chunk-count below)
     ("final", 800, 800, 200, [120, 400, 700], 0, None),              # Next-Week final (media, instances)
 ]
 
@@ -62,6 +64,49 @@ def test_config_band_full_spp(name, W, H, spp, rows, x0, w, earth):
     assert st.segments == cnt["segments"], (name, st.segments, cnt["segments"])
     linf = float(np.abs(img - ref).max())
     assert linf <= TOL, (name, linf)
+
+
+@pytest.mark.gpu
+def test_c5_cornell_2048_10000spp_bands(earth):
+    """BASELINE config 5 at its own sample count: Cornell 2048^2 at 10000 spp (application.rs:639-721 scene,
+    :443-456 sample loop).  A general scene splits a pixel's samples into 8 chunks (lane.h sample_chunk:
+    1250 samples each, summed in order, then reduce_chunks adds the 8 partials in chunk order), so each
+    chunk sum runs over 1250 f32 additions and the pixel over 10000 samples in total.  Two 256-px bands,
+    through the boxes (row 300) and under the light (row 1900), rendered as tiles of the full frame."""
+    W, H, spp, rows, x0, w = 2048, 2048, 10000, [300, 1900], 896, 256
+    img, st = _gpu_rows("cornell", W, H, spp, rows, earth, x0, w)
+    o = O.OracleScene(hrt.PRESETS["cornell"], 1, earth)
+    ref, cnt = o.render_rows(W, H, spp, rows, 50, seed=1, threads=THREADS, x0=x0, w=w, task_w=8)
+    assert st.samples == cnt["samples"] == len(rows) * w * spp
+    assert st.segments == cnt["segments"], (st.segments, cnt["segments"])
+    linf = float(np.abs(img - ref).max())
+    print(f"C5 10000 spp: {len(rows)} x {w} px, rays {st.segments}, L-inf {linf:.3e}")
+    assert linf <= TOL, linf
+
+
+@pytest.mark.gpu
+def test_device_built_walk_vs_oracle(earth):
+    """A scene of 39.9k leaves (random_40k: the Random builder over a 200 x 200 grid) takes the
+    device-side build of the walk hierarchy by default (build_walk.hip, >= 32768 leaves); its frame band
+    against the oracle's recursive BvhNode walk of the same scene."""
+    import torch
+
+    W, H, spp, rows, x0, w = 1920, 1080, 64, [300, 540], 640, 512
+    s = hrt.preset("random_40k", 1, earth)
+    s.commit()
+    si = s.scene_info()
+    assert si.walk_device_built == 1 and si.walk_regrouped == 1
+    cam = hrt.preset_camera(s.info, W, H)
+    p = hrt.params(W, H, spp, 50, 1, tuple(s.info.background))
+    d = torch.empty(len(rows) * w * 4, dtype=torch.float32, device="cuda")
+    st = hrt.render_tiles_device(s, cam, p, [(x0, y, w, 1) for y in rows], d.data_ptr(), 0, want_stats=True)
+    img = d.view(len(rows), w, 4).cpu().numpy()
+    ref, cnt = O.OracleScene(hrt.PRESETS["random_40k"], 1, earth).render_rows(W, H, spp, rows, 50, seed=1,
+                                                                            threads=THREADS, x0=x0, w=w, task_w=8)
+    assert st.segments == cnt["segments"], (st.segments, cnt["segments"])
+    linf = float(np.abs(img - ref).max())
+    print(f"random_40k ({si.prims} prims, device build {si.walk_build_us} us): rays {st.segments}, L-inf {linf:.3e}")
+    assert linf <= TOL, linf
 
 
 @pytest.mark.gpu

@@ -71,6 +71,63 @@ def test_tile_split_and_gather_match_single_process(world):
     assert segs == cnt["segments"]
 
 
+STEPS = 4
+
+
+def _delivery_worker(rank, world, port, q):
+    """bench.py's per-frame delivery (hrt/delivery.py): every step a different frame (seed SEED + k), each
+    rank's share submitted as it would be after its launch, rank 0 receiving every completed frame."""
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "hyper-ray-tracer_amd"), root]
+    import hrt
+    from hrt import delivery, tiling
+    from oracle import oracle as O
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    o = O.OracleScene(hrt.PRESETS["random"], 1)
+    tiles = tiling.split_tiles(W, H, world, rank, 16)
+    shares = []
+    for k in range(STEPS):
+        parts = [o.render(W, H, SPP, DEPTH, seed=SEED + k, region=t, threads=2)[0].reshape(-1) for t in tiles]
+        shares.append(np.concatenate(parts))
+    got = {}
+    fd = delivery.FrameDelivery(W, H, world, rank, tiles, on_frame=lambda k, f: got.__setitem__(k, f.copy()))
+    dist.barrier()
+    for k in range(STEPS):
+        fd.submit(k, shares[k])
+    fd.flush(STEPS)
+    dist.barrier()
+    fd.close()
+    if rank == 0:
+        q.put(got)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_pipelined_frame_delivery_matches_single_process(world):
+    """The shared-memory delivery (double-buffered frames, a worker thread per rank) hands rank 0 every
+    step's frame, each equal bit for bit to the single-process frame of that step."""
+    import hrt
+    from oracle import oracle as O
+
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    pc = mp.start_processes(_delivery_worker, args=(world, _free_port(), q), nprocs=world, join=False,
+                            start_method="spawn")
+    got = q.get()
+    while not pc.join(timeout=60):
+        pass
+    o = O.OracleScene(hrt.PRESETS["random"], 1)
+    assert sorted(got) == list(range(STEPS))
+    for k in range(STEPS):
+        ref, _ = o.render(W, H, SPP, DEPTH, seed=SEED + k, threads=4)
+        assert np.array_equal(got[k], ref), k
+
+
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
 def test_split_is_a_balanced_partition(world):
     from hrt import tiling
