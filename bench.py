@@ -123,10 +123,11 @@ SCENE_DATA = {
 }
 
 
-def log(msg):
+def log(msg, all_ranks=False):
     """Progress on stderr (stdout carries only the JSON line)."""
-    if int(os.environ.get("RANK", "0")) == 0:
-        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+    rank = int(os.environ.get("RANK", "0"))
+    if rank == 0 or all_ranks:
+        print(f"[bench r{rank}] {msg}", file=sys.stderr, flush=True)
 
 
 def band_rows(H, n):
@@ -265,7 +266,9 @@ def delivery_phase(args, scene, cam, p, tiles, n_px, dev, stream, world, rank, b
         if k == K:  # the last timed frame (step 0 is the untimed warm-up through the pipeline)
             last["frame"] = f.copy()
 
+    log("delivery phase: set-up", all_ranks=True)
     fd = delivery.FrameDelivery(W, H, world, rank, tiles, on_frame=keep, device=dev)
+    log("delivery phase: running", all_ranks=True)
     try:
         for k in range(K + 1):
             if k == 1:  # step 0 warmed the pipeline (pinned pages, placement index, shared frame)
@@ -277,6 +280,7 @@ def delivery_phase(args, scene, cam, p, tiles, n_px, dev, stream, world, rank, b
             hrt.render_tiles_device(scene, cam, p, tiles, outs[k % 2].data_ptr(), stream.cuda_stream)
             fd.submit(k, outs[k % 2], stream)
         fd.flush(K + 1)
+        log(f"delivery phase: {K + 1} frames delivered", all_ranks=True)
         barrier()
         dt = time.perf_counter() - t0
         if world > 1:
@@ -368,6 +372,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     scene.synchronize()  # raises if the walk watchdog stopped any timed launch (incomplete frame)
+    log(f"timed steps done: {dt / args.steps * 1e3:.1f} ms per step", all_ranks=True)
     launch_ms = sum(a.elapsed_time(b) for a, b in ev) / max(1, args.steps)
     rank_ms = [round(launch_ms, 2)]
     if world > 1:

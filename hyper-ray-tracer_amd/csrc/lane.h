@@ -433,6 +433,11 @@ struct PathKey {
  * `winner` = node index of the accepted leaf (NONE if nothing).  MEDIA: ConstantMedium nodes are
  * evaluated (their boundary walks are nested calls with MEDIA = false). */
 template <int CULL, bool FULL, bool MEDIA, bool COUNT, bool FAST = false>
+HRT_LANE void trace_ray(const KParams& P, const G::Node* __restrict__ nodes, const G::Prim* __restrict__ prims,
+                        uint32_t begin, uint32_t end, TRay r, float tmin, float& closest, uint32_t& winner,
+                        const PathKey& pk, Counts& cn);
+
+template <int CULL, bool FULL, bool MEDIA, bool COUNT, bool FAST = false>
 HRT_LANE void trace(const KParams& P, const G::Node* __restrict__ nodes, const G::Prim* __restrict__ prims,
                       uint32_t begin, uint32_t end, Vec3 o, Vec3 d, float time, float tmin, float& closest,
                       uint32_t& winner, const PathKey& pk, Counts& cn) {
@@ -443,7 +448,16 @@ HRT_LANE void trace(const KParams& P, const G::Node* __restrict__ nodes, const G
     begin = oct * P.stream_len;
     end = begin + P.stream_len;
   }
-  const Vec3 base_o = o, base_d = d; /* the ray this walk started with */
+  trace_ray<CULL, FULL, MEDIA, COUNT, FAST>(P, nodes, prims, begin, end, r, tmin, closest, winner, pk, cn);
+}
+
+/* The walk over [begin, end) of the node stream with a set-up ray r (its o, d are the frame the walk
+ * starts in: instance ends re-derive their parent frame from them). */
+template <int CULL, bool FULL, bool MEDIA, bool COUNT, bool FAST>
+HRT_LANE void trace_ray(const KParams& P, const G::Node* __restrict__ nodes, const G::Prim* __restrict__ prims,
+                        uint32_t begin, uint32_t end, TRay r, float tmin, float& closest, uint32_t& winner,
+                        const PathKey& pk, Counts& cn) {
+  const Vec3 base_o = r.o, base_d = r.d; /* the ray this walk started with */
   uint32_t i = begin;
   while (i < end) {
     const G::Node* np = nodes + i;
@@ -1150,6 +1164,31 @@ HRT_LANE_FI void walk_prim(const KParams& P, const WalkSrc& src, uint32_t& i, co
   const uint32_t leaf = i - WALK_PEND; /* the leaf's payload */
   i = walk_successor<MEM>(src, leaf); /* the walk goes on at the leaf's pre-order successor */
   walk_leaf_test<COUNT, MEM>(P, src, leaf, r, closest, winner, cn);
+}
+
+/* A passed leaf of the GENERAL walk stream (layout.h): the reference test of the enclosing BvhNode box
+ * (box-less leaves, GL_BOX), then the leaf's program -- its range of the reference stream, whose first
+ * node is the leaf's own box (the reference test at the leaf) -- from the world ray
+ * against the lane's current closest.  The winner is a reference-stream node index (make_record<true>). */
+template <bool MEDIA, bool COUNT, int MEM>
+HRT_LANE_FI void gwalk_leaf_test(const KParams& P, const G::Node* __restrict__ nodes, const G::Prim* __restrict__ prims,
+                                 const WalkSrc& src, uint32_t leaf, const TRay& r, float& closest, uint32_t& winner,
+                                 const PathKey& pk, Counts& cn) {
+  const float4 h = wload<MEM>(src, leaf);
+  if (f2u(h.z) & G::GL_BOX) {
+    const float4 bmn = wload<MEM>(src, leaf + 16u), bmx = wload<MEM>(src, leaf + 32u);
+    if (!box_ref(bmn, bmx, r, P.t_min, closest)) return;
+  }
+  trace_ray<G::CULL_EXACT, true, MEDIA, COUNT>(P, nodes, prims, f2u(h.x), f2u(h.y), r, P.t_min, closest, winner, pk, cn);
+}
+
+template <bool MEDIA, bool COUNT, int MEM>
+HRT_LANE_FI void gwalk_prim(const KParams& P, const G::Node* __restrict__ nodes, const G::Prim* __restrict__ prims,
+                            const WalkSrc& src, uint32_t& i, const TRay& r, float& closest, uint32_t& winner,
+                            const PathKey& pk, Counts& cn) {
+  const uint32_t leaf = i - WALK_PEND;
+  i = walk_successor<MEM>(src, leaf);
+  gwalk_leaf_test<MEDIA, COUNT, MEM>(P, nodes, prims, src, leaf, r, closest, winner, pk, cn);
 }
 
 /* both halves back to back (the host lane simulator's walk) */

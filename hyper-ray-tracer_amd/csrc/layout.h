@@ -186,5 +186,23 @@ constexpr uint32_t WALK_NODE_BYTES = 32, WALK_PAYLOAD_BYTES = 96;
 constexpr uint32_t WL_MOVING = 1u, WL_NOBOX = 2u;
 enum : uint32_t { WT_SOLID = 0, WT_CHECKER = 1, WT_GLOBAL = 2 }; /* inline texture of a leaf's material */
 
+/* ---------------------------------------------------------------- general-scene walk stream
+ * What render_gwalk_kernel walks under CULL_EXACT for scenes with rects, instances, media and every
+ * texture (scene.cpp build_gwalk).  The node parts are the sphere stream's; the leaves are the LEAF
+ * OBJECTS of the reference stream, in its pre-order: the smallest pieces the reference's BvhNode
+ * hierarchy hands to a non-BVH hittable -- a BvhNode leaf (K_BOX_PRIM, or a K_BOX whose subtree holds no
+ * box outside an instance: an instance chain, a Cuboid, a List, a ConstantMedium), or a box-less List
+ * member.  A leaf's PROGRAM is its range [begin, end) of the reference node stream, run by lane.h
+ * trace_ray from the world ray (the leaf's own box node first: the reference test at the leaf).  Leaf
+ * payload (GWALK_PAYLOAD_BYTES):
+ *   float4(begin, end, flags, w)     w = successor << 2 (walk_successor, as in the sphere stream)
+ *   float4(mn.xyz, 0) float4(mx.xyz, 0)   GL_BOX: the nearest enclosing BvhNode box of a box-less leaf,
+ *                                         whose reference test (aabb.rs) precedes the program
+ * The node part's C, E box holds the leaf's geometry (its reference box, or for a transposed ZX rect
+ * (G17) that box joined with the rect's true extent; E = +inf when no finite box is known), so the
+ * inflated test culls only what cannot hold an accepted hit. */
+constexpr uint32_t GWALK_PAYLOAD_BYTES = 48;
+constexpr uint32_t GL_BOX = 1u;
+
 }  // namespace gpu
 }  // namespace hrt

@@ -351,6 +351,9 @@ constexpr size_t LDS_GEN_MAX = 48 * 1024;
 
 struct Plan {
   bool full, fast, lds;
+  bool gwalk;    /* general scene on render_gwalk_kernel (the general walk stream, render_general.hip) */
+  int gwalk_mem; /* its walk-stream placement: WM_LDS / WM_HYB / WM_BUF */
+  bool gwalk_lref; /* ... with the reference stream and primitives staged in LDS too */
   int gen_waves; /* general scenes under CULL_EXACT: the render_kernel<FULL> instantiation (3 or 4 waves/SIMD) */
   int trim;      /* general scenes: features compiled out of render_kernel (lane.h TRIM_*) */
   bool general; /* sphere scene forced onto the general kernel (diagnostics: HRT_KERNEL=general) */
@@ -396,12 +399,36 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
   if ((s->feature_mask & (G::F_NOISE | G::F_IMAGE)) == 0)
     pl.trim = TRIM_HEAVY_TEX | ((s->feature_mask & G::F_MEDIUM) == 0 && !s->media_nested ? TRIM_MEDIA : 0);
   if (lt && strcmp(lt, "0") == 0) pl.trim = 0;
+  /* General scenes under exact culling: render_gwalk_kernel over the general walk stream (persistent
+   * walks, postponed shading, batched leaf programs) unless HRT_KERNEL asks for a segment kernel. */
+  pl.gwalk = pl.full && s->w_general && s->w_end > 0 && pl.cull == G::CULL_EXACT && !s->media_nested &&
+             !(k && (strcmp(k, "general") == 0 || strcmp(k, "persistent") == 0 || strcmp(k, "segment") == 0));
+  pl.gwalk_mem = WM_BUF;
+  pl.gwalk_lref = false;
+  if (pl.gwalk) {
+    pl.general = false;
+    const size_t walk = s->w_hot ? s->w_hot : s->w_end;
+    const size_t ref = s->g_nodes.size() * sizeof(G::Node) + s->g_prims.size() * sizeof(G::Prim);
+    const bool no_lds = (flags & HRT_RENDER_NO_LDS) != 0;
+    pl.gwalk_mem = no_lds || walk > LDS_SCENE_MAX ? WM_BUF : (s->w_hot ? WM_HYB : WM_LDS);
+    const char* lr = getenv("HRT_GWALK_LREF"); /* A/B knob: "0" keeps the reference stream in global memory */
+    pl.gwalk_lref = pl.gwalk_mem == WM_LDS && walk + ref <= LDS_SCENE_MAX && !(lr && strcmp(lr, "0") == 0);
+    pl.smem = pl.gwalk_mem == WM_BUF ? 0 : walk + (pl.gwalk_lref ? ref : 0);
+    pl.lds = pl.gwalk_mem != WM_BUF;
+    pl.trim = ((s->feature_mask & (G::F_NOISE | G::F_IMAGE)) == 0 ? TRIM_HEAVY_TEX : 0) |
+              ((s->feature_mask & G::F_MEDIUM) == 0 ? TRIM_MEDIA : 0);
+    if (lt && strcmp(lt, "0") == 0) pl.trim = 0;
+  }
   return pl;
 }
 
 template <bool COUNT>
 void launch_any(const hrt_scene* s, const Plan& pl, const KParams& kp, hipStream_t stream) {
   const size_t smem = pl.lds ? pl.smem : 0;
+  if (pl.gwalk) {
+    launch_gwalk(COUNT, pl.gwalk_mem, pl.gwalk_lref, pl.trim, kp, s->device, stream, smem);
+    return;
+  }
   if (pl.fast) {
     if (pl.lds) launch<G::CULL_SLAB, false, COUNT, true, true>(kp, s->device, stream, smem);
     else launch<G::CULL_SLAB, false, COUNT, false, true>(kp, s->device, stream, 0);
@@ -497,8 +524,8 @@ KParams scene_params(const hrt_scene* s, const hrt_camera* cam, const hrt_render
    * of postpone {40..56} x batch {4, 6, 8}: C2 best at 52-56 / 4, random-10k at 44 / 4, +1.8% over 48 / 6;
    * DESIGN.md section 10) */
   const bool spec = !pl.full && !pl.general && !pl.fast && pl.cull == G::CULL_EXACT;
-  kp.postpone = env_knob("HRT_POSTPONE", spec ? (s->w_hot ? 44 : 52) : 56);
-  kp.prim_batch = env_knob("HRT_PRIM_BATCH", spec ? 4 : 8);
+  kp.postpone = env_knob("HRT_POSTPONE", pl.gwalk ? 44 : (spec ? (s->w_hot ? 44 : 52) : 56));
+  kp.prim_batch = env_knob("HRT_PRIM_BATCH", (spec || pl.gwalk) ? 4 : 8);
   /* a walk visits each node at most once, a medium's boundary subtree at most twice per medium node */
   kp.walk_cap = 3u * (uint32_t)s->g_nodes.size() + 64u;
   kp.motion_uniform = s->motion_uniform ? 1u : 0u;
@@ -507,7 +534,8 @@ KParams scene_params(const hrt_scene* s, const hrt_camera* cam, const hrt_render
   kp.walk = base + s->off_walk;
   kp.walk_bytes = s->w_end;
   kp.walk_end = s->w_end;
-  kp.walk_hot = pl.lds && !pl.full && !pl.fast && pl.cull == G::CULL_EXACT ? s->w_hot : 0;
+  kp.walk_hot = (pl.gwalk && pl.gwalk_mem == WM_HYB) || (pl.lds && !pl.full && !pl.fast && pl.cull == G::CULL_EXACT)
+                    ? s->w_hot : 0;
   return kp;
 }
 
@@ -760,7 +788,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
      * segment kernels claim per lane: a segment iteration is long, claims are rare, and with few items
      * per lane (Cornell 1024^2 x 128: 2) blocks unbalance the waves (-6%).
      * HRT_CLAIM_FINE (A/B knob): claim the last that many items per lane, in every kernel */
-    const bool sphere_kernel = !pl.full && !pl.fast && !pl.general;
+    const bool sphere_kernel = (!pl.full && !pl.fast && !pl.general) || pl.gwalk; /* block claims */
     const char* cf = getenv("HRT_CLAIM_FINE");
     const uint64_t fine = cf ? strtoull(cf, nullptr, 10) : (sphere_kernel ? 0u : pad);
     kp.claim_fine = (uint32_t)(pad > fine ? pad - fine : 0);

@@ -1,0 +1,255 @@
+/*
+ * render_general.hip — the general-scene kernel with persistent walks (render_gwalk_kernel): rects,
+ * instances, media, lights and every texture (Cornell, Cornell-smoke, Final, Earth+Perlin, ...).
+ *
+ * It is render_basic_kernel's schedule (render_sphere.hip) over the GENERAL walk
+ * stream (layout.h): the wave steps its lanes' walks one node at a time over a re-grouped hierarchy of the
+ * reference's leaf objects, leaves a passed leaf's test pending while the lane walks on (speculative walk),
+ * runs the pending tests of many lanes in one batched block, and shades once enough lanes have finished.
+ * A leaf's test is its PROGRAM: the leaf's range of the reference node stream (its BvhNode box, instance
+ * brackets, a Cuboid's or a List's primitives, a ConstantMedium's boundary walks) run by lane.h trace_ray
+ * from the world ray against the lane's closest, so every state that instances and media need lives inside
+ * that block and the walk loop keeps the sphere kernel's registers.  Shading is the segment kernels'
+ * shade<true> (hit record through the instance chain, emission, scatter, textures).
+ *
+ * Each lane runs exactly the reference's sequence of world.hit calls and RNG draws (a lane's tests are in
+ * the reference's leaf order with its closest; tests/test_lane_sim.py holds the lane to the oracle and to
+ * render_full_kernel's lane bit for bit), so the image is the segment kernel's.
+ */
+#include "kernel_common.h"
+
+using namespace hrt;
+using namespace hrt::lane;
+using namespace hrt::kern;
+
+#ifndef HRT_GWALK_WAVES
+#define HRT_GWALK_WAVES 4
+#endif
+
+namespace {
+
+constexpr int GWALK_WAVES = HRT_GWALK_WAVES;
+
+/* WMEM: where the walk stream is read (WM_LDS: staged whole; WM_HYB: its top levels staged, the rest
+ * through the buffer descriptor; WM_BUF: global memory).  LREF: the reference node stream and the
+ * primitives that leaf programs read are staged in LDS behind the walk stream. */
+template <bool COUNT, int WMEM, bool LREF, int TRIM>
+__global__ __launch_bounds__(128 * GWALK_WAVES, GWALK_WAVES)
+void render_gwalk_kernel(KParams P) {
+  extern __shared__ float4 lds_scene[];
+  constexpr bool MEDIA = !(TRIM & TRIM_MEDIA);
+  const G::Node* nodes = P.nodes;
+  const G::Prim* prims = P.prims;
+  const uint32_t lds_base = (uint32_t)(size_t)(__attribute__((address_space(3))) float4*)lds_scene;
+  WalkSrc ws;
+  ws.base = P.walk;
+  ws.hot = P.walk_hot;
+#if defined(__HIP_DEVICE_COMPILE__)
+  ws.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)P.walk, 0, (int)P.walk_bytes, 0x00020000);
+#endif
+  uint32_t staged = 0; /* bytes of the walk stream in LDS, at LDS address 0 */
+  if constexpr (WMEM == WM_LDS || WMEM == WM_HYB) {
+    staged = WMEM == WM_HYB ? P.walk_hot : P.walk_bytes;
+    const float4* g = reinterpret_cast<const float4*>(P.walk);
+    for (uint32_t k = threadIdx.x; k < staged / 16u; k += blockDim.x) lds_scene[k] = g[k];
+  }
+  if constexpr (LREF) { /* the reference stream and primitives behind it (16-B aligned: the stream is) */
+    const uint32_t n4 = P.n_nodes * (uint32_t)(sizeof(G::Node) / 16), p4 = P.n_prims * (uint32_t)(sizeof(G::Prim) / 16);
+    float4* dst = lds_scene + staged / 16u;
+    const float4* gn = reinterpret_cast<const float4*>(P.nodes);
+    const float4* gp = reinterpret_cast<const float4*>(P.prims);
+    for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) dst[k] = gn[k];
+    for (uint32_t k = threadIdx.x; k < p4; k += blockDim.x) dst[n4 + k] = gp[k];
+    nodes = reinterpret_cast<const G::Node*>(dst);
+    prims = reinterpret_cast<const G::Prim*>(dst + n4);
+  }
+  __syncthreads();
+  if ((WMEM == WM_LDS || WMEM == WM_HYB) && lds_base != 0u) { /* stream offsets are LDS addresses */
+    if (threadIdx.x == 0) atomicOr(&P.stats[12], 2ull);
+    return;
+  }
+  uint32_t* const slot_lds = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(lds_scene) + P.lane_lds) + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  const float scale = 1.0f / (float)P.spp; /* application.rs:403 */
+  const float inf = __uint_as_float(0x7f800000u);
+  const uint32_t end = P.walk_end;
+  const float tmin_c = __builtin_canonicalizef(P.t_min);
+  const uint32_t need = P.postpone;
+  const uint32_t batch = P.prim_batch;
+  const uint32_t cap = P.walk_cap * 128u;
+
+  bool has_item = false, exhausted = false;
+  bool walking = false, setup = false;
+  Item it{0u, 0u, 0u, 0u};
+  WaveBlock wb{0u, 0u};
+  Vec3 sum = v3(0.0f, 0.0f, 0.0f);
+  PathState ps;
+  init_path_state(ps);
+  TRay r;
+  set_ray(r, ps.ro, ps.rd, 0.0f, P);
+  uint32_t node = G::NONE, winner = G::NONE, pend = G::NONE;
+  float closest = inf;
+  uint32_t n_seg = 0, n_samples = 0, n_pixels = 0;
+  Counts cn{0u, 0u, 0u, 0u, 0u, 0u};
+  PhaseClock pc{{0ull, 0ull, 0ull}, 0ull};
+  auto stamp = [&](int phase) {
+    if constexpr (COUNT) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (phase >= 0) pc.cyc[phase] += t - pc.last;
+      pc.last = t;
+    }
+  };
+  stamp(-1);
+
+  for (;;) {
+    const bool had_item = has_item;
+    claim_work(P, lane, has_item, exhausted, it, wb);
+    if (has_item && !had_item) *slot_lds = it.slot;
+    if (!__any(has_item || !exhausted)) break;
+    if (has_item && !walking) {
+      start_sample(P, ps, it.pxy & 0xFFFFu, it.pxy >> 16, it.sample);
+      walking = true;
+      setup = true;
+    }
+    if (setup) {
+      set_ray(r, ps.ro, ps.rd, ps.rtime, P);
+      closest = inf;
+      winner = G::NONE;
+      node = ps.depth_left == 0 ? G::NONE : 0u; /* max_depth 0: black without a world.hit (:478-480) */
+      setup = false;
+    }
+    if constexpr (COUNT) cn.shade_slots++;
+    stamp(0);
+    const unsigned long long walkers = __ballot(walking);
+    uint32_t iters = 0;
+    bool stuck = false;
+    for (;;) {
+#pragma unroll
+      for (int u = 0; u < WALK_UNROLL; u++) {
+        if constexpr (COUNT) cn.walk_slots++;
+        if (node < end) {
+          walk_box<COUNT, WMEM>(ws, node, r, tmin_c, closest, cn);
+        } else if constexpr (COUNT) {
+          if (walk_pending(node)) cn.park_slots++;
+          else if (walking) cn.wait_slots++;
+        }
+        if ((u + 1) % PRIM_EVERY != 0) continue;
+        /* speculative walk (render_sphere.hip): a passed leaf's program waits in `pend` while the lane
+         * walks on; the wave runs the pending programs once `batch` lanes are blocked or none can step */
+        if (walk_pending(node) && pend == G::NONE) {
+          pend = node - WALK_PEND;
+          node = walk_successor<WMEM>(ws, pend);
+        }
+        const bool waiting = pend != G::NONE && !(node < end);
+        const unsigned long long pm = __ballot(waiting);
+        if (pm && ((uint32_t)__popcll(pm) >= batch || !__ballot(node < end))) {
+          if constexpr (COUNT) cn.prim_slots++;
+          if (pend != G::NONE) {
+            gwalk_leaf_test<MEDIA, COUNT, WMEM>(P, nodes, prims, ws, pend, r, closest, winner, ps.pk, cn);
+            pend = G::NONE;
+            if (walk_pending(node)) {
+              pend = node - WALK_PEND;
+              node = walk_successor<WMEM>(ws, pend);
+            }
+          }
+        }
+      }
+      const unsigned long long live = __ballot(node < end || walk_pending(node) || pend != G::NONE);
+      if (!live || (uint32_t)__popcll(walkers & ~live) >= need) break;
+      if (++iters > cap) { stuck = true; break; }
+    }
+    if (stuck) {
+      if (lane == 0) atomicOr(&P.stats[12], 1ull);
+      exhausted = true;
+      has_item = false;
+      walking = false;
+      node = G::NONE;
+      pend = G::NONE;
+    }
+    stamp(1);
+    /* shade the finished segments (application.rs:483-494) */
+    const bool shading = walking && node >= end && !walk_pending(node) && pend == G::NONE;
+    const bool traced = shading && node != G::NONE;
+    bool sample_done = false, chunk_done = false;
+    if (shading) {
+      bool done = true;
+      if (traced) {
+        ps.pk.segment++;
+        done = shade<true, COUNT, TRIM>(P, ps, winner, closest, r.o, r.d, r.time, r.tau, cn) || ps.depth_left == 0;
+      }
+      if (done) {
+        walking = false;
+        node = G::NONE;
+        sum = sum + ps.rad; /* application.rs:448: samples of a chunk summed in order */
+        sample_done = true;
+        if (++it.sample == it.sample_end) {
+          if (P.n_chunks == 1)
+            P.out[*slot_lds] = make_float4(sqrtf(sum.x * scale), sqrtf(sum.y * scale), sqrtf(sum.z * scale), 1.0f);
+          else
+            P.partial[*slot_lds] = make_float4(sum.x, sum.y, sum.z, 0.0f);
+          chunk_done = true;
+          has_item = false;
+          sum = v3(0.0f, 0.0f, 0.0f);
+        }
+      } else {
+        setup = true; /* the scattered ray keeps the sample's shutter time */
+        node = G::NONE;
+      }
+    }
+    n_seg += (uint32_t)__popcll(__ballot(traced));
+    n_samples += (uint32_t)__popcll(__ballot(sample_done));
+    n_pixels += (uint32_t)__popcll(__ballot(chunk_done && it.sample_end <= P.chunk));
+    stamp(2);
+  }
+  if (lane == 0) {
+    atomicAdd(&P.stats[0], (unsigned long long)n_seg);
+    atomicAdd(&P.stats[1], (unsigned long long)n_samples);
+    atomicAdd(&P.stats[2], (unsigned long long)n_pixels);
+  }
+  if constexpr (COUNT) {
+    flush_counts(P, cn);
+    if (lane == 0)
+      for (int k = 0; k < 3; k++) atomicAdd(&P.stats[9 + k], pc.cyc[k]);
+  }
+}
+
+template <bool COUNT, int WMEM, bool LREF, int TRIM>
+void launch_g(const KParams& kp, int device, hipStream_t stream, size_t smem) {
+  const void* fn = (const void*)render_gwalk_kernel<COUNT, WMEM, LREF, TRIM>;
+  const int block = 128 * GWALK_WAVES;
+  KParams p = kp;
+  p.lane_lds = (uint32_t)((smem + 15) & ~(size_t)15);
+  const size_t total = p.lane_lds + (size_t)block * sizeof(uint32_t);
+  const int grid = resident_grid(fn, block, device, total, true);
+  hipLaunchKernelGGL((render_gwalk_kernel<COUNT, WMEM, LREF, TRIM>), dim3(grid), dim3(block), total, stream, p);
+  hip_check(hipGetLastError(), "render_gwalk_kernel launch");
+}
+
+template <bool COUNT, int TRIM>
+void launch_g_mem(int wmem, bool lref, const KParams& kp, int device, hipStream_t stream, size_t smem) {
+  if (wmem == WM_LDS) lref ? launch_g<COUNT, WM_LDS, true, TRIM>(kp, device, stream, smem)
+                           : launch_g<COUNT, WM_LDS, false, TRIM>(kp, device, stream, smem);
+  else if (wmem == WM_HYB) launch_g<COUNT, WM_HYB, false, TRIM>(kp, device, stream, smem);
+  else launch_g<COUNT, WM_BUF, false, TRIM>(kp, device, stream, smem);
+}
+
+}  // namespace
+
+namespace hrt {
+
+void launch_gwalk(bool count, int wmem, bool lref, int trim, const KParams& kp, int device, hipStream_t stream,
+                  size_t smem) {
+  if (count) {
+    if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX)) launch_g_mem<true, TRIM_MEDIA | TRIM_HEAVY_TEX>(wmem, lref, kp, device, stream, smem);
+    else if (trim == TRIM_MEDIA) launch_g_mem<true, TRIM_MEDIA>(wmem, lref, kp, device, stream, smem);
+    else if (trim == TRIM_HEAVY_TEX) launch_g_mem<true, TRIM_HEAVY_TEX>(wmem, lref, kp, device, stream, smem);
+    else launch_g_mem<true, 0>(wmem, lref, kp, device, stream, smem);
+  } else {
+    if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX)) launch_g_mem<false, TRIM_MEDIA | TRIM_HEAVY_TEX>(wmem, lref, kp, device, stream, smem);
+    else if (trim == TRIM_MEDIA) launch_g_mem<false, TRIM_MEDIA>(wmem, lref, kp, device, stream, smem);
+    else if (trim == TRIM_HEAVY_TEX) launch_g_mem<false, TRIM_HEAVY_TEX>(wmem, lref, kp, device, stream, smem);
+    else launch_g_mem<false, 0>(wmem, lref, kp, device, stream, smem);
+  }
+}
+
+}  // namespace hrt

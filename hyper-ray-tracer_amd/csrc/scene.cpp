@@ -729,7 +729,8 @@ namespace hrt {
 void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::vector<WalkLeaf>& leaves) {
   const uint32_t N = (uint32_t)T.size();
   uint64_t total = 0;
-  for (const WNode& w : T) total += G::WALK_NODE_BYTES + (w.leaf >= 0 ? G::WALK_PAYLOAD_BYTES : 0);
+  const uint32_t PB = s->w_general ? G::GWALK_PAYLOAD_BYTES : G::WALK_PAYLOAD_BYTES;
+  for (const WNode& w : T) total += G::WALK_NODE_BYTES + (w.leaf >= 0 ? PB : 0);
   need(total < (1ull << 30), HRT_ERR_UNSUPPORTED, "scene too large for the walk stream");
   std::vector<uint32_t> addr(N), paddr(N, 0);
   const char* hot_env = getenv("HRT_WALK_HOT"); /* "0": no LDS-staged top levels (A/B) */
@@ -755,13 +756,13 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
     }
     if (T[i].leaf >= 0 && !hot[i]) {
       paddr[i] = off;
-      off += G::WALK_PAYLOAD_BYTES;
+      off += PB;
     }
   }
   for (uint32_t i = 0; i < N; i++)
     if (T[i].leaf >= 0 && hot[i]) {
       paddr[i] = off;
-      off += G::WALK_PAYLOAD_BYTES;
+      off += PB;
     }
   need(off == total, HRT_ERR_STATE, "walk stream placement");
   const uint32_t END = off;
@@ -784,12 +785,23 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
     const WalkLeaf& L = leaves[w.leaf];
     put4(o, addr[i], C[0], C[1], C[2], u2f(skip));
     put4(o, addr[i] + 16, E[0], E[1], E[2], u2f(paddr[i] | G::WALK_PEND));
+    if (s->w_general) { /* layout.h general-scene walk stream: the leaf's program range */
+      const uint32_t q = paddr[i];
+      put4(o, q, u2f(L.begin), u2f(L.end), u2f(L.has_rbox ? G::GL_BOX : 0u), u2f(skip << 2));
+      put4(o, q + 16, L.rbox.mn.x, L.rbox.mn.y, L.rbox.mn.z, 0.0f);
+      put4(o, q + 32, L.rbox.mx.x, L.rbox.mx.y, L.rbox.mx.z, 0.0f);
+      continue;
+    }
     const G::Prim& p = s->g_prims[L.prim];
     const bool moving = (p.km & 3u) == G::P_MOVING;
-    const uint32_t wflags = (moving ? G::WL_MOVING : 0u) | (L.nobox ? G::WL_NOBOX : 0u) | (skip << 2);
+    /* the reference test at the leaf: its own box, or for a box-less List member the nearest enclosing
+     * BvhNode box (monotone: it implies every enclosing box's test), or none at world level */
+    const bool ref_test = !L.nobox || L.has_rbox;
+    const Aabb& rb = L.nobox ? L.rbox : L.box;
+    const uint32_t wflags = (moving ? G::WL_MOVING : 0u) | (ref_test ? 0u : G::WL_NOBOX) | (skip << 2);
     const uint32_t q = paddr[i];
-    put4(o, q, L.box.mn.x, L.box.mn.y, L.box.mn.z, u2f(wflags));
-    put4(o, q + 16, L.box.mx.x, L.box.mx.y, L.box.mx.z, p.p0[3]);
+    put4(o, q, rb.mn.x, rb.mn.y, rb.mn.z, u2f(wflags));
+    put4(o, q + 16, rb.mx.x, rb.mx.y, rb.mx.z, p.p0[3]);
     put4(o, q + 32, p.p0[0], p.p0[1], p.p0[2], moving ? p.p1[3] : 0.0f);
     put4(o, q + 48, moving ? p.p1[0] : 0.0f, moving ? p.p1[1] : 0.0f, moving ? p.p1[2] : 0.0f, moving ? p.p2[0] : 1.0f);
     /* the material, inline (layout.h) */
@@ -848,10 +860,165 @@ std::vector<WalkLeaf> walk_leaves(const hrt_scene* s, std::vector<WNode>* ref_tr
     L.prim = g.kp & 0xFFFFFFu;
     L.box = b;
     if (L.nobox) ok = false;
+    if (L.nobox && !open.empty()) { /* a List member inside a BvhNode leaf: that box's reference test */
+      L.has_rbox = true;
+      L.rbox = T[open.back()].box;
+    }
     for (int k = 0; k < 3 && !L.nobox; k++)
       if (!(g.mn[k] <= g.mx[k]) || !std::isfinite(g.mn[k]) || !std::isfinite(g.mx[k])) ok = false;
     T.push_back(WNode{b, (int32_t)leaves.size(), i + 1, (uint32_t)open.size()});
     leaves.push_back(L);
+  }
+  if (ref_tree) *ref_tree = std::move(T);
+  if (regroup_ok) *regroup_ok = ok;
+  return leaves;
+}
+
+/* The general stream's leaf objects (layout.h) in the reference's pre-order, and the reference
+ * hierarchy above them (WNode ends as reference-stream indices: the caller renumbers).  A K_BOX is a
+ * hierarchy node when its subtree holds a box node outside every instance bracket (its children are
+ * BvhNodes); otherwise it is a leaf, its program the whole subtree (boxes inside instances included:
+ * trace_ray walks them in the instance's frame). */
+std::vector<WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<WNode>* ref_tree, bool* regroup_ok) {
+  const uint32_t n = s->main_end;
+  const float inf = u2f(0x7f800000u);
+  std::vector<WalkLeaf> leaves;
+  std::vector<WNode> T;
+  std::vector<uint32_t> start; /* reference-stream index at which each hierarchy node starts */
+  struct Open { uint32_t end; Aabb box; };
+  std::vector<Open> open;
+  bool ok = true;
+  auto node_box = [&](uint32_t i) {
+    const G::Node& g = s->g_nodes[i];
+    Aabb b;
+    b.mn = v3(g.mn[0], g.mn[1], g.mn[2]);
+    b.mx = v3(g.mx[0], g.mx[1], g.mx[2]);
+    return b;
+  };
+  auto finite_box = [](const Aabb& b) {
+    for (int k = 0; k < 3; k++)
+      if (!(b.mn[k] <= b.mx[k]) || !std::isfinite(b.mn[k]) || !std::isfinite(b.mx[k])) return false;
+    return true;
+  };
+  /* the true extent of a world-level sphere or rect (rect.rs:55-59 axes: a ZX rect spans z over
+   * [a0, a1] and x over [b0, b1], the transpose of its bounding box, G17) */
+  auto prim_extent = [&](uint32_t prim, Aabb& b) {
+    const G::Prim& p = s->g_prims[prim];
+    if (p.parent != G::NONE) return false;
+    const uint32_t kind = p.km & 3u;
+    if (kind == G::P_SPHERE) {
+      b.mn = v3(p.p0[0] - p.p0[3], p.p0[1] - p.p0[3], p.p0[2] - p.p0[3]);
+      b.mx = v3(p.p0[0] + p.p0[3], p.p0[1] + p.p0[3], p.p0[2] + p.p0[3]);
+      return finite_box(b);
+    }
+    if (kind != G::P_RECT) return false;
+    const uint32_t plane = (p.km >> 2) & 3u;
+    const int ka = plane == HRT_PLANE_XY ? 2 : (plane == HRT_PLANE_YZ ? 0 : 1);
+    const int aa = plane == HRT_PLANE_XY ? 0 : (plane == HRT_PLANE_YZ ? 1 : 2);
+    const int ba = plane == HRT_PLANE_XY ? 1 : (plane == HRT_PLANE_YZ ? 2 : 0);
+    float mn[3], mx[3];
+    mn[ka] = mx[ka] = p.p1[0];
+    mn[aa] = p.p0[0]; mx[aa] = p.p0[1];
+    mn[ba] = p.p0[2]; mx[ba] = p.p0[3];
+    b.mn = v3(mn[0], mn[1], mn[2]);
+    b.mx = v3(mx[0], mx[1], mx[2]);
+    return finite_box(b);
+  };
+  auto add_leaf = [&](uint32_t begin, uint32_t end, bool has_box, const Aabb& box, bool ref_only, int prim) {
+    WalkLeaf L;
+    L.begin = begin;
+    L.end = end;
+    L.prim = prim >= 0 ? (uint32_t)prim : G::NONE;
+    L.nobox = true;
+    Aabb ext;
+    const bool has_ext = prim >= 0 && prim_extent((uint32_t)prim, ext);
+    if (has_box && !ref_only) { /* a BvhNode box that holds its geometry (box_ok) */
+      L.box = box;
+      L.nobox = false;
+    } else if (has_ext) { /* a world-level primitive: its extent (joined with its transposed box) */
+      L.box = has_box ? box_union(box, ext) : ext;
+      L.nobox = false;
+    }
+    if (!L.nobox && !finite_box(L.box)) L.nobox = true;
+    if (L.nobox) {
+      ok = false;
+      L.box.mn = v3(-inf, -inf, -inf);
+      L.box.mx = v3(inf, inf, inf);
+    }
+    if (!has_box && !open.empty()) { /* box-less: the nearest enclosing BvhNode's reference test first */
+      L.has_rbox = true;
+      L.rbox = open.back().box;
+    }
+    T.push_back(WNode{L.box, (int32_t)leaves.size(), end, (uint32_t)open.size()});
+    start.push_back(begin);
+    leaves.push_back(L);
+  };
+  uint32_t i = 0;
+  while (i < n) {
+    while (!open.empty() && open.back().end <= i) open.pop_back();
+    const G::Node& g = s->g_nodes[i];
+    const uint32_t kind = (g.kp >> 24) & G::KIND_MASK, payload = g.kp & 0xFFFFFFu;
+    const bool ref_only = (g.kp & G::NODE_REF_ONLY) != 0;
+    if (kind == G::K_BOX) {
+      const uint32_t skip = g.skip;
+      need(skip > i && skip <= n, HRT_ERR_STATE, "general walk stream: bad skip link");
+      bool hierarchy = false;
+      int depth = 0;
+      for (uint32_t j = i + 1; j < skip && !hierarchy; j++) {
+        const uint32_t k = (s->g_nodes[j].kp >> 24) & G::KIND_MASK;
+        if (k == G::K_INST_BEGIN) depth++;
+        else if (k == G::K_INST_END) depth--;
+        else if (depth == 0 && (k == G::K_BOX || k == G::K_BOX_PRIM)) hierarchy = true;
+      }
+      if (hierarchy) {
+        T.push_back(WNode{node_box(i), -1, skip, (uint32_t)open.size()});
+        start.push_back(i);
+        open.push_back(Open{skip, node_box(i)});
+        i++;
+        continue;
+      }
+      /* the leaf's single primitive, if the subtree is one world-level prim (for its true extent) */
+      const int prim = (skip == i + 2 && ((s->g_nodes[i + 1].kp >> 24) & G::KIND_MASK) == G::K_PRIM)
+                           ? (int)(s->g_nodes[i + 1].kp & 0xFFFFFFu) : -1;
+      add_leaf(i, skip, true, node_box(i), ref_only, prim);
+      i = skip;
+    } else if (kind == G::K_BOX_PRIM) {
+      add_leaf(i, i + 1, true, node_box(i), ref_only, (int)payload);
+      i++;
+    } else if (kind == G::K_PRIM) {
+      add_leaf(i, i + 1, false, Aabb{}, false, (int)payload);
+      i++;
+    } else if (kind == G::K_INST_BEGIN) { /* a box-less instance chain: up to its matching end */
+      int depth = 0;
+      uint32_t j = i;
+      for (; j < n; j++) {
+        const uint32_t k = (s->g_nodes[j].kp >> 24) & G::KIND_MASK;
+        if (k == G::K_INST_BEGIN) depth++;
+        else if (k == G::K_INST_END && --depth == 0) break;
+      }
+      need(j < n, HRT_ERR_STATE, "general walk stream: unbalanced instance brackets");
+      add_leaf(i, j + 1, false, Aabb{}, false, -1);
+      i = j + 1;
+    } else if (kind == G::K_MEDIUM) {
+      add_leaf(i, i + 1, false, Aabb{}, false, -1);
+      i++;
+    } else {
+      need(false, HRT_ERR_STATE, "general walk stream: unbalanced instance brackets");
+    }
+  }
+  /* ends: reference-stream indices -> hierarchy indices (the first node starting at or after the end) */
+  for (size_t k = 0; k < T.size(); k++) {
+    size_t m = k + 1;
+    while (m < T.size() && start[m] < T[k].end) m++;
+    T[k].end = (uint32_t)m;
+  }
+  /* an inner node's box for the inflated test: the union of its children's (a BvhNode box is the union
+   * of its children's REFERENCE boxes, which for a transposed ZX rect (G17) need not hold the rect) */
+  for (size_t k = T.size(); k-- > 0;) {
+    if (T[k].leaf >= 0) continue;
+    Aabb u = T[k + 1].box;
+    for (uint32_t c = T[k + 1].end; c < T[k].end; c = T[c].end) u = box_union(u, T[c].box);
+    T[k].box = u;
   }
   if (ref_tree) *ref_tree = std::move(T);
   if (regroup_ok) *regroup_ok = ok;
@@ -865,7 +1032,26 @@ void build_walk(hrt_scene* s) {
   s->w_regrouped = false;
   s->w_device_built = false;
   s->w_regroup_pending = false;
-  if ((s->feature_mask & ~G::F_BASIC) != 0) return; /* sphere scenes only */
+  s->w_general = false;
+  if ((s->feature_mask & ~G::F_BASIC) != 0) { /* general scenes: the leaf-object stream (layout.h) */
+    const char* gw = getenv("HRT_GWALK"); /* "0": no general walk stream (segment kernels only) */
+    if ((gw && strcmp(gw, "0") == 0) || s->media_nested) return;
+    std::vector<WNode> T;
+    bool regroup_ok = false;
+    const std::vector<WalkLeaf> leaves = gwalk_leaves(s, &T, &regroup_ok);
+    if (leaves.empty()) return;
+    s->w_general = true;
+    const char* mode = getenv("HRT_WALK_TREE");
+    if (regroup_ok && !(mode && strcmp(mode, "reference") == 0)) {
+      const auto t0 = std::chrono::steady_clock::now();
+      T.clear();
+      walk_regroup(T, leaves);
+      s->w_build_us = (uint32_t)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+      s->w_regrouped = true;
+    }
+    walk_place_and_write(s, T, leaves);
+    return;
+  }
   std::vector<WNode> T;
   bool regroup_ok = false;
   const std::vector<WalkLeaf> leaves = walk_leaves(s, &T, &regroup_ok);

@@ -65,9 +65,14 @@ struct HMat {
 /* the sphere kernel's walk stream (layout.h): a leaf of the reference stream, and the hierarchy the
  * stream encodes, in pre-order (a node's subtree is [i, end)) */
 struct WalkLeaf {
-  Aabb box;
-  bool nobox;
+  Aabb box;   /* holds the leaf's geometry (sphere stream: the reference box) */
+  bool nobox; /* no such box: the inflated test always passes */
   uint32_t prim;
+  /* general stream (layout.h): the leaf's program [begin, end) of the reference stream, and the
+   * enclosing BvhNode box a box-less leaf is tested against first */
+  uint32_t begin = 0, end = 0;
+  bool has_rbox = false;
+  Aabb rbox{};
 };
 struct WNode {
   Aabb box;     /* inner: the union of its leaves' boxes */
@@ -113,6 +118,7 @@ struct hrt_scene {
   bool w_regrouped = false;  /* inner boxes re-grouped over the reference leaf order (build_walk) */
   bool w_device_built = false; /* ... by the device-side build (build_walk.hip) */
   bool w_regroup_pending = false; /* re-grouping left to the device build at upload */
+  bool w_general = false;    /* the stream is the general-scene walk stream (layout.h; build_gwalk) */
   uint32_t w_build_us = 0;   /* time of the re-grouping (host or device) */
   size_t off_walk = 0;
   uint32_t feature_mask = 0;
@@ -160,6 +166,8 @@ std::vector<uint8_t> build_blob(hrt_scene* s); /* scene.cpp: the arrays in one b
  * and the placement + records of a hierarchy over them */
 std::vector<host::WalkLeaf> walk_leaves(const hrt_scene* s, std::vector<host::WNode>* ref_tree, bool* regroup_ok);
 void walk_place_and_write(hrt_scene* s, const std::vector<host::WNode>& T, const std::vector<host::WalkLeaf>& leaves);
+/* scene.cpp: the general-scene walk stream's leaf objects (layout.h) in the reference's pre-order */
+std::vector<host::WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<host::WNode>* ref_tree, bool* regroup_ok);
 /* build_walk.hip: the re-grouped hierarchy (scene.cpp walk_regroup's splits) built on the device */
 void device_walk_regroup(const std::vector<host::WalkLeaf>& leaves, std::vector<host::WNode>& T, int device);
 void device_release(hrt_scene* s);

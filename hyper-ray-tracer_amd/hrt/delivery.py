@@ -35,7 +35,7 @@ import numpy as np
 from . import tiling
 
 HDR_BYTES = 4096
-WAIT_S = 300.0  # longest any wait may take before the delivery declares itself stuck (raises)
+WAIT_S = 120.0  # longest any wait may take before the delivery declares itself stuck (raises)
 
 
 def share_index(width: int, tiles: Sequence[tiling.Tile]) -> Optional[np.ndarray]:
@@ -138,7 +138,9 @@ class FrameDelivery:
 
     def flush(self, n: int) -> None:
         target = (lambda: self.delivered >= n) if self.rank == 0 else (lambda: self.placed >= n)
-        _wait(lambda: target() or self.err is not None, "the last frame")
+        _wait(lambda: target() or self.err is not None or self.hdr[self.world + 1] != 0, f"frame {n - 1}")
+        if self.hdr[self.world + 1] != 0 and not self.err:
+            self.err = RuntimeError("another rank's frame delivery failed")
         if self.err:
             raise self.err
 
@@ -187,6 +189,11 @@ class FrameDelivery:
                     hdr[self.world] = k + 1
                     self.delivered = k + 1
         except BaseException as e:  # surfaced by submit / flush on the main thread
+            import sys
+            import traceback
+
+            print(f"[delivery rank {self.rank}] worker failed: {e!r}", file=sys.stderr, flush=True)
+            traceback.print_exc(file=sys.stderr)
             self.err = e
             try:
                 self.hdr[self.world + 1] = 1

@@ -79,7 +79,7 @@ step() {
     rehearsal)
       local tag=$1; shift
       echo "== $tag: 2-rank rehearsal $*" >> "$LOG"
-      timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+      timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29533 bench.py --gpus 2 --one-device "$@" >> "$OUT/$tag.jsonl" 2>> "$OUT/$tag.err"
       local rc=$?; echo "== $tag exit $rc" >> "$LOG"; return $rc ;;
     configs)

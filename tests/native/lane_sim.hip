@@ -21,7 +21,8 @@ using namespace hrt::lane;
 
 namespace {
 
-/* KIND 0: render_basic_kernel's lane, 1: render_full_kernel's lane, 2: render_kernel's (segment()) */
+/* KIND 0: render_basic_kernel's lane, 1: render_full_kernel's lane, 2: render_kernel's (segment()),
+ * 3: render_gwalk_kernel's (the general walk stream) */
 template <int CULL, int KIND>
 void render_pixel(const KParams& P, uint32_t px, uint32_t py, float* rgba, uint64_t* cnt) {
   constexpr bool FULL = KIND == 1;
@@ -53,7 +54,22 @@ void render_pixel(const KParams& P, uint32_t px, uint32_t py, float* rgba, uint6
       Vec3 wo = ps.ro, wd = ps.rd;
       for (;;) {
         bool traced, done;
-        if constexpr (FULL) {
+        if constexpr (KIND == 3) { /* render_gwalk_kernel: the general walk stream, leaf programs, shade<true> */
+          uint32_t node = ps.depth_left == 0 ? G::NONE : 0u, winner = G::NONE;
+          float closest = inf;
+          WalkSrc src;
+          src.base = P.walk;
+          while (node < P.walk_end) {
+            walk_box<true, WM_HOST>(src, node, r, P.t_min, closest, cn);
+            if (walk_pending(node)) gwalk_prim<true, true, WM_HOST>(P, P.nodes, P.prims, src, node, r, closest, winner, ps.pk, cn);
+          }
+          traced = node != G::NONE;
+          done = true;
+          if (traced) {
+            ps.pk.segment++;
+            done = shade<true, true>(P, ps, winner, closest, r.o, r.d, r.time, r.tau, cn) || ps.depth_left == 0;
+          }
+        } else if constexpr (FULL) {
           FullWalk w{0u, P.main_end, 0u, 0u, P.t_min, inf, G::NONE, inf, 0.0f, G::NONE};
           if (ps.depth_left == 0) w.i = G::NONE;
           while (w.i < w.end) full_step<CULL, true>(P, P.nodes, P.prims, w, r, wo, wd, ps.pk, cn);
@@ -110,7 +126,7 @@ void render_pixel(const KParams& P, uint32_t px, uint32_t py, float* rgba, uint6
 extern "C" {
 
 /* kernel: 0 = render_basic_kernel's lane, 1 = render_full_kernel's, 2 = render_kernel's (segment
- * at a time); cull: layout.h CULL_*.
+ * at a time), 3 = render_gwalk_kernel's (general walk stream; CULL_EXACT); cull: layout.h CULL_*.
  * cnt[0..4] += segments, samples, node visits, primitive tests, texture evaluations. */
 int lane_sim_render(const void* blob, const hrt_blob_info* bi, const hrt_camera* cam, const hrt_render_params* p,
                     int kernel, int cull, uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, float* rgba,
@@ -155,6 +171,7 @@ int lane_sim_render(const void* blob, const hrt_blob_info* bi, const hrt_camera*
   P.background = v3(p->background[0], p->background[1], p->background[2]);
   P.seed = p->seed;
   if (kernel == 0 && (bi->feature_mask & ~G::F_BASIC) != 0) return 1; /* not a sphere scene */
+  if (kernel == 3 && ((bi->feature_mask & ~G::F_BASIC) == 0 || bi->walk_bytes == 0)) return 1; /* no general stream */
   for (uint32_t y = 0; y < h; y++)
     for (uint32_t x = 0; x < w; x++) {
       float* o = rgba + 4 * ((size_t)y * w + x);
@@ -166,6 +183,8 @@ int lane_sim_render(const void* blob, const hrt_blob_info* bi, const hrt_camera*
         if (cull == G::CULL_EXACT) render_pixel<G::CULL_EXACT, 1>(P, x0 + x, y0 + y, o, cnt);
         else if (cull == G::CULL_SLAB) render_pixel<G::CULL_SLAB, 1>(P, x0 + x, y0 + y, o, cnt);
         else render_pixel<G::CULL_REFERENCE, 1>(P, x0 + x, y0 + y, o, cnt);
+      } else if (kernel == 3) {
+        render_pixel<G::CULL_EXACT, 3>(P, x0 + x, y0 + y, o, cnt);
       } else {
         if (cull == G::CULL_EXACT) render_pixel<G::CULL_EXACT, 2>(P, x0 + x, y0 + y, o, cnt);
         else if (cull == G::CULL_SLAB) render_pixel<G::CULL_SLAB, 2>(P, x0 + x, y0 + y, o, cnt);

@@ -200,19 +200,82 @@ def _has_gpu():
 @pytest.mark.skipif(not _has_gpu(), reason="needs a GPU")
 @pytest.mark.parametrize("name,w,h,spp", [("cornell", 40, 40, 16), ("cornell_smoke", 40, 40, 16), ("final", 40, 40, 8),
                                           ("features", 64, 36, 16), ("earth_perlin", 48, 27, 16), ("simple_light", 48, 27, 16)])
-def test_persistent_general_kernel_equals_segment_kernel(earth, monkeypatch, name, w, h, spp):
-    """render_full_kernel (HRT_KERNEL=persistent) against the default segment-at-a-time kernel: the
-    per-lane code is shared (csrc/lane.h, host-checked by tests/test_lane_sim.py), so the images must be
-    identical bit for bit."""
+def test_general_kernels_are_bit_identical(earth, monkeypatch, name, w, h, spp):
+    """The default general-scene kernel, render_gwalk_kernel (the general walk stream: persistent walks,
+    batched leaf programs), against the segment-at-a-time kernel (HRT_KERNEL=segment) and render_full_kernel
+    (HRT_KERNEL=persistent): the per-lane code is shared (csrc/lane.h, host-checked by
+    tests/test_lane_sim.py), so the images must be identical bit for bit.  The default is the walk-stream
+    kernel: only it and the sphere kernel run batched leaf blocks (prim_slots > 0)."""
     s = hrt.preset(name, 1, earth)
     s.commit()
     cam = hrt.preset_camera(s.info, w, h)
     p = hrt.params(w, h, spp, 50, 7, tuple(s.info.background))
     a, sa = hrt.render(s, cam, p, stats=True)
-    monkeypatch.setenv("HRT_KERNEL", "persistent")
-    b, sb = hrt.render(s, cam, p, stats=True)
-    assert sa.segments == sb.segments
-    assert np.array_equal(a, b)
+    pc = hrt.params(w, h, spp, 50, 7, tuple(s.info.background), flags=hrt.RENDER_COUNT_WORK)
+    c, sc = hrt.render(s, cam, pc, stats=True)
+    assert sc.prim_slots > 0 and np.array_equal(a, c)
+    for kernel in ("segment", "persistent"):
+        monkeypatch.setenv("HRT_KERNEL", kernel)
+        b, sb = hrt.render(s, cam, p, stats=True)
+        assert sa.segments == sb.segments, kernel
+        assert np.array_equal(a, b), kernel
+        monkeypatch.delenv("HRT_KERNEL")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,W,H,spp", [("cornell", 96, 80, 70), ("final", 64, 48, 40)])
+def test_general_walk_kernel_tiles_and_chunks(earth, monkeypatch, name, W, H, spp):
+    """render_gwalk_kernel on a multi-tile call (ragged 16-px tiles of a 3-way split, packed back to back)
+    and with sample chunks (spp > 32: several chunk sums per pixel): every share equals the whole frame's
+    pixels, and the frame equals the segment kernel's."""
+    import torch
+
+    from hrt import tiling
+
+    s = hrt.preset(name, 1, earth)
+    s.commit()
+    cam = hrt.preset_camera(s.info, W, H)
+    p = hrt.params(W, H, spp, 50, 5, tuple(s.info.background))
+    full, st = hrt.render(s, cam, p, stats=True)
+    frame = np.full((H, W, 4), np.nan, np.float32)
+    segs = 0
+    for r in range(3):
+        t = tiling.split_tiles(W, H, 3, r)
+        d = torch.empty(tiling.share_pixels(t) * 4, dtype=torch.float32, device="cuda")
+        sr = hrt.render_tiles_device(s, cam, p, t, d.data_ptr(), 0, want_stats=True)
+        segs += int(sr.segments)
+        tiling.place_tiles(frame, t, d.cpu().numpy())
+    assert segs == st.segments and np.array_equal(frame, full)
+    monkeypatch.setenv("HRT_KERNEL", "segment")
+    seg, ss = hrt.render(s, cam, p, stats=True)
+    assert ss.segments == st.segments and np.array_equal(seg, full)
+
+
+@pytest.mark.gpu
+def test_general_walk_watchdog(earth):
+    """Corrupt skip links in the general walk stream (every inner record's fail link -> the root) make walks
+    loop; render_gwalk_kernel's watchdog stops them and the frame is reported HRT_ERR_STATE."""
+    s = hrt.preset("final", 1, earth)
+    s.commit()
+    W, H = 48, 32
+    cam = hrt.preset_camera(s.info, W, H)
+    p = hrt.params(W, H, 2, 50, 3, tuple(s.info.background))
+    hrt.render(s, cam, p)  # intact scene first
+    buf, info = hrt.scene_blob(s)
+    assert info.walk_bytes > 0
+    ws = np.frombuffer(buf.raw, np.uint32, count=info.walk_bytes // 4, offset=info.off_walk).copy()
+    off, inner = 0, 0
+    while off < info.walk_bytes:
+        leaf = (ws[off // 4 + 7] & 0x80000000) != 0
+        if not leaf:
+            ws[off // 4 + 3] = 0
+            inner += 1
+        off += 80 if leaf else 32  # layout.h WALK_NODE_BYTES (+ GWALK_PAYLOAD_BYTES)
+    assert inner > 100
+    s.poke_blob(info.off_walk, ws.tobytes())
+    with pytest.raises(hrt.HrtError) as e:
+        hrt.render(s, cam, p)
+    assert e.value.status == hrt.ERR_STATE
 
 
 @pytest.mark.gpu

@@ -176,3 +176,30 @@ def test_walk_stream_regrouped_equals_reference_hierarchy(sim, earth, name, monk
     if name != "two_spheres":  # (two leaves: nothing to re-group)
         assert sa["nodes"] < 0.95 * sb["nodes"], (sa["nodes"], sb["nodes"])
     print(name, "node visits: re-grouped", sa["nodes"], "reference hierarchy", sb["nodes"])
+
+
+GENERAL_CASES = [c for c in CASES if c[0] not in BASIC_SCENES]
+
+
+@pytest.mark.parametrize("name,w,h,spp,depth", GENERAL_CASES)
+def test_general_walk_lane_matches_oracle_and_general_lane(sim, earth, name, w, h, spp, depth):
+    """render_gwalk_kernel's lane: the general walk stream (leaf objects of the reference stream under a
+    re-grouped hierarchy, layout.h) with each passed leaf's program run from the world ray.  Held to the
+    oracle, and bit for bit to render_full_kernel's lane (same tests in the same order, same shading)."""
+    img, st = sim_render(sim, name, w, h, spp, depth, 3, earth, kernel=3, cull=CULL_EXACT)
+    ref, cnt = oracle_render(name, w, h, spp, depth, 3, earth)
+    assert st["segments"] == cnt["segments"]
+    assert np.abs(img - ref).max() <= TOL
+    full, sf = sim_render(sim, name, w, h, spp, depth, 3, earth, kernel=1, cull=CULL_EXACT)
+    assert np.array_equal(img, full) and st["segments"] == sf["segments"]
+    print(name, "primitive tests: general walk", st["prims"], "full lane", sf["prims"])
+
+
+@pytest.mark.parametrize("name", ["cornell", "final", "features", "cornell_smoke", "simple_light"])
+def test_general_walk_stream_regrouped_equals_reference_hierarchy(sim, earth, name, monkeypatch):
+    a, sa = sim_render(sim, name, 32, 24, 4, 50, 5, earth, kernel=3, cull=CULL_EXACT)
+    monkeypatch.setenv("HRT_WALK_TREE", "reference")
+    b, sb = sim_render(sim, name, 32, 24, 4, 50, 5, earth, kernel=3, cull=CULL_EXACT)
+    assert sa["segments"] == sb["segments"] and sa["prims"] == sb["prims"]
+    assert np.array_equal(a, b)
+    print(name, "node visits: re-grouped", sa["nodes"], "reference hierarchy", sb["nodes"])
