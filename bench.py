@@ -311,7 +311,17 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("gloo")  # control plane + host gather only (no RCCL, no device collective)
+        # control plane + host gather only (no RCCL, no device collective).  Gloo prints its connection
+        # report on stdout, which carries only the JSON line: send fd 1 to stderr meanwhile.
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo")
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     if args.one_device:
         local = 0
     torch.cuda.set_device(local)
@@ -401,7 +411,7 @@ def main():
                                       ms_per_step=dt / args.steps * 1e3)
     if world > 1 and tiled:
         tg = time.perf_counter()
-        if frame is None:
+        if deliv is None:  # no delivery phase: gather the last timed frame's shares over gloo
             frame = tiling.gather_frame(out.cpu().numpy(), W, H, world, rank,
                                         shares=lambda r: tiling.split_tiles(W, H, world, r, args.tile))
         gather_s = time.perf_counter() - tg

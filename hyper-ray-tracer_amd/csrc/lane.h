@@ -1175,11 +1175,31 @@ HRT_LANE_FI void gwalk_leaf_test(const KParams& P, const G::Node* __restrict__ n
                                  const WalkSrc& src, uint32_t leaf, const TRay& r, float& closest, uint32_t& winner,
                                  const PathKey& pk, Counts& cn) {
   const float4 h = wload<MEM>(src, leaf);
-  if (f2u(h.z) & G::GL_BOX) {
-    const float4 bmn = wload<MEM>(src, leaf + 16u), bmx = wload<MEM>(src, leaf + 32u);
+  const uint32_t flags = f2u(h.z);
+  if (!(flags & (G::GL_BOX | G::GL_INST))) {
+    trace_ray<G::CULL_EXACT, true, MEDIA, COUNT>(P, nodes, prims, f2u(h.x), f2u(h.y), r, P.t_min, closest, winner, pk, cn);
+    return;
+  }
+  const float4 bmn = wload<MEM>(src, leaf + 16u);
+  if (flags & G::GL_BOX) {
+    const float4 bmx = wload<MEM>(src, leaf + 32u);
     if (!box_ref(bmn, bmx, r, P.t_min, closest)) return;
   }
-  trace_ray<G::CULL_EXACT, true, MEDIA, COUNT>(P, nodes, prims, f2u(h.x), f2u(h.y), r, P.t_min, closest, winner, pk, cn);
+  if (!(flags & G::GL_INST)) {
+    trace_ray<G::CULL_EXACT, true, MEDIA, COUNT>(P, nodes, prims, f2u(h.x), f2u(h.y), r, P.t_min, closest, winner, pk, cn);
+    return;
+  }
+  /* a leaf of a flattened instance chain (layout.h GL_INST): the ray in the innermost instance's frame,
+   * as the reference's Translation / Rotation hits hand it down (apply_chain), with 1/d and d.d of the
+   * turned direction where the program reads them */
+  TRay lr = r;
+  apply_chain(P, f2u(bmn.w), lr.o, lr.d);
+  if (flags & G::GL_INV) lr.inv = v3(1.0f / lr.d.x, 1.0f / lr.d.y, 1.0f / lr.d.z);
+  if (flags & G::GL_DD) {
+    lr.dd = dot(lr.d, lr.d);
+    lr.rdd = div_rn_y(lr.dd);
+  }
+  trace_ray<G::CULL_EXACT, true, MEDIA, COUNT>(P, nodes, prims, f2u(h.x), f2u(h.y), lr, P.t_min, closest, winner, pk, cn);
 }
 
 template <bool MEDIA, bool COUNT, int MEM>

@@ -196,13 +196,20 @@ enum : uint32_t { WT_SOLID = 0, WT_CHECKER = 1, WT_GLOBAL = 2 }; /* inline textu
  * trace_ray from the world ray (the leaf's own box node first: the reference test at the leaf).  Leaf
  * payload (GWALK_PAYLOAD_BYTES):
  *   float4(begin, end, flags, w)     w = successor << 2 (walk_successor, as in the sphere stream)
- *   float4(mn.xyz, 0) float4(mx.xyz, 0)   GL_BOX: the nearest enclosing BvhNode box of a box-less leaf,
- *                                         whose reference test (aabb.rs) precedes the program
+ *   float4(mn.xyz, inst) float4(mx.xyz, 0)   GL_BOX: the nearest enclosing BvhNode box of a box-less leaf
+ *                                         (world frame), whose reference test (aabb.rs) precedes the program
+ * Instance chains are flattened: each leaf object inside a Translation / Rotation (a primitive, a Cuboid,
+ * a leaf of the instance's own BvhNode) is a leaf of the stream, its box the chain's image of its geometry.
  * The node part's C, E box holds the leaf's geometry (its reference box, or for a transposed ZX rect
  * (G17) that box joined with the rect's true extent; E = +inf when no finite box is known), so the
  * inflated test culls only what cannot hold an accepted hit. */
 constexpr uint32_t GWALK_PAYLOAD_BYTES = 48;
-constexpr uint32_t GL_BOX = 1u;
+/* leaf flags (payload word 2).  A leaf inside a Translation / Rotation chain (GL_INST: the innermost
+ * instance in word 7) runs its program in that instance's frame: the world ray through the chain (lane.h
+ * apply_chain, the reference's own operations), with 1/d (GL_INV: boxes below) and d.d (GL_DD: spheres
+ * below) recomputed when the chain turns the direction (GL_DIR).  Its GL_BOX box is then the nearest
+ * world-frame BvhNode box around the chain; boxes inside the instance are tested by the program itself. */
+constexpr uint32_t GL_BOX = 1u, GL_INST = 2u, GL_DIR = 4u, GL_INV = 8u, GL_DD = 16u;
 
 }  // namespace gpu
 }  // namespace hrt

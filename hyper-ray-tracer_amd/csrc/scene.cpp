@@ -787,8 +787,8 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
     put4(o, addr[i] + 16, E[0], E[1], E[2], u2f(paddr[i] | G::WALK_PEND));
     if (s->w_general) { /* layout.h general-scene walk stream: the leaf's program range */
       const uint32_t q = paddr[i];
-      put4(o, q, u2f(L.begin), u2f(L.end), u2f(L.has_rbox ? G::GL_BOX : 0u), u2f(skip << 2));
-      put4(o, q + 16, L.rbox.mn.x, L.rbox.mn.y, L.rbox.mn.z, 0.0f);
+      put4(o, q, u2f(L.begin), u2f(L.end), u2f((L.has_rbox ? G::GL_BOX : 0u) | L.gflags), u2f(skip << 2));
+      put4(o, q + 16, L.rbox.mn.x, L.rbox.mn.y, L.rbox.mn.z, u2f(L.inst));
       put4(o, q + 32, L.rbox.mx.x, L.rbox.mx.y, L.rbox.mx.z, 0.0f);
       continue;
     }
@@ -902,9 +902,8 @@ std::vector<WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<WNode>* ref_t
   };
   /* the true extent of a world-level sphere or rect (rect.rs:55-59 axes: a ZX rect spans z over
    * [a0, a1] and x over [b0, b1], the transpose of its bounding box, G17) */
-  auto prim_extent = [&](uint32_t prim, Aabb& b) {
+  auto prim_extent = [&](uint32_t prim, Aabb& b) { /* in the primitive's own frame */
     const G::Prim& p = s->g_prims[prim];
-    if (p.parent != G::NONE) return false;
     const uint32_t kind = p.km & 3u;
     if (kind == G::P_SPHERE) {
       b.mn = v3(p.p0[0] - p.p0[3], p.p0[1] - p.p0[3], p.p0[2] - p.p0[3]);
@@ -923,6 +922,102 @@ std::vector<WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<WNode>* ref_t
     b.mn = v3(mn[0], mn[1], mn[2]);
     b.mx = v3(mx[0], mx[1], mx[2]);
     return finite_box(b);
+  };
+  /* the world image of a box in instance `inst`'s frame: its corners through the chain back to the world
+   * (innermost first, the inverse of lane.h inst_ray, in double), padded for the f32 rounding of the
+   * reference's ray transforms */
+  auto to_world = [&](const Aabb& b, uint32_t inst, Aabb& out) {
+    double mn[3] = {1e300, 1e300, 1e300}, mx[3] = {-1e300, -1e300, -1e300}, scale = 0.0;
+    for (int c = 0; c < 8; c++) {
+      double p[3] = {(c & 1) ? b.mx.x : b.mn.x, (c & 2) ? b.mx.y : b.mn.y, (c & 4) ? b.mx.z : b.mn.z};
+      for (int k = 0; k < 3; k++) scale = std::max(scale, std::fabs(p[k]));
+      for (uint32_t q = inst; q != G::NONE; q = s->g_insts[q].parent) {
+        const G::Inst& in = s->g_insts[q];
+        if ((in.kind & G::I_KIND_MASK) == G::I_TRANSLATE) {
+          for (int k = 0; k < 3; k++) p[k] += (double)in.d[k];
+        } else {
+          const int a = (int)(in.axis + 1) % 3, bb = (int)(in.axis + 2) % 3;
+          const double sn = in.sin_t, cs = in.cos_t, pa = p[a], pb = p[bb];
+          p[a] = cs * pa - sn * pb;
+          p[bb] = sn * pa + cs * pb;
+        }
+        for (int k = 0; k < 3; k++) scale = std::max(scale, std::fabs(p[k]));
+      }
+      for (int k = 0; k < 3; k++) {
+        mn[k] = std::min(mn[k], p[k]);
+        mx[k] = std::max(mx[k], p[k]);
+      }
+    }
+    const double pad = 1e-5 * scale + 1e-30;
+    float fmn[3], fmx[3];
+    for (int k = 0; k < 3; k++) {
+      fmn[k] = (float)(mn[k] - pad);
+      fmx[k] = (float)(mx[k] + pad);
+      if ((double)fmn[k] > mn[k] - pad) fmn[k] = nextafterf(fmn[k], -3.40282347e+38f);
+      if ((double)fmx[k] < mx[k] + pad) fmx[k] = nextafterf(fmx[k], 3.40282347e+38f);
+    }
+    out.mn = v3(fmn[0], fmn[1], fmn[2]);
+    out.mx = v3(fmx[0], fmx[1], fmx[2]);
+    return finite_box(out);
+  };
+  /* Flatten the instance chains of a leaf object's content [a, b) (layout.h): every leaf object inside
+   * (a primitive, a box-less Cuboid / List member, a BvhNode leaf or box-only subtree of the instance's
+   * own hierarchy) becomes a leaf with its chain.  Not possible (false) when a box sits in an outer frame
+   * of a nested instance, a box-less primitive sits under a box of its frame, or a medium is inside. */
+  struct Flat { uint32_t begin, end, inst; bool has_box; Aabb box; bool ref_only; int prim; };
+  auto flatten_chains = [&](uint32_t a, uint32_t b, std::vector<Flat>& out) {
+    std::vector<uint32_t> insts, local_end;
+    for (uint32_t j = a; j < b;) {
+      while (!local_end.empty() && local_end.back() <= j) local_end.pop_back();
+      const G::Node& g = s->g_nodes[j];
+      const uint32_t k = (g.kp >> 24) & G::KIND_MASK, pl = g.kp & 0xFFFFFFu;
+      const bool ro = (g.kp & G::NODE_REF_ONLY) != 0;
+      const uint32_t inst = insts.empty() ? G::NONE : insts.back();
+      if (k == G::K_INST_BEGIN) {
+        if (!local_end.empty()) return false;
+        insts.push_back(pl);
+        j++;
+      } else if (k == G::K_INST_END) {
+        if (!local_end.empty() || insts.empty()) return false;
+        insts.pop_back();
+        j++;
+      } else if (k == G::K_BOX) {
+        if (insts.empty()) return false;
+        bool has_inst = false, has_box = false;
+        for (uint32_t m = j + 1; m < g.skip; m++) {
+          const uint32_t km = (s->g_nodes[m].kp >> 24) & G::KIND_MASK;
+          has_inst |= km == G::K_INST_BEGIN || km == G::K_MEDIUM;
+          has_box |= km == G::K_BOX || km == G::K_BOX_PRIM;
+        }
+        if (has_inst) return false;
+        if (has_box) { /* a hierarchy node of the instance's BvhNode: implied by its leaves' own tests */
+          local_end.push_back(g.skip);
+          j++;
+          continue;
+        }
+        const int prim = (g.skip == j + 2 && ((s->g_nodes[j + 1].kp >> 24) & G::KIND_MASK) == G::K_PRIM)
+                             ? (int)(s->g_nodes[j + 1].kp & 0xFFFFFFu) : -1;
+        Aabb bx;
+        bx.mn = v3(g.mn[0], g.mn[1], g.mn[2]);
+        bx.mx = v3(g.mx[0], g.mx[1], g.mx[2]);
+        out.push_back(Flat{j, g.skip, inst, true, bx, ro, prim});
+        j = g.skip;
+      } else if (k == G::K_BOX_PRIM) {
+        if (insts.empty()) return false;
+        Aabb bx;
+        bx.mn = v3(g.mn[0], g.mn[1], g.mn[2]);
+        bx.mx = v3(g.mx[0], g.mx[1], g.mx[2]);
+        out.push_back(Flat{j, j + 1, inst, true, bx, ro, (int)pl});
+        j++;
+      } else if (k == G::K_PRIM) {
+        if (!local_end.empty()) return false;
+        out.push_back(Flat{j, j + 1, inst, false, Aabb{}, false, (int)pl});
+        j++;
+      } else {
+        return false; /* a medium */
+      }
+    }
+    return insts.empty();
   };
   auto add_leaf = [&](uint32_t begin, uint32_t end, bool has_box, const Aabb& box, bool ref_only, int prim) {
     WalkLeaf L;
@@ -953,6 +1048,49 @@ std::vector<WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<WNode>* ref_t
     start.push_back(begin);
     leaves.push_back(L);
   };
+  /* a leaf of a flattened chain: its program in the frame of `f.inst`, after the reference test of the
+   * world-frame box `wbox` around the chain (if any) */
+  auto add_flat = [&](const Flat& f, bool has_wbox, const Aabb& wbox, uint32_t ref_end) {
+    WalkLeaf L;
+    L.begin = f.begin;
+    L.end = f.end;
+    L.prim = f.prim >= 0 ? (uint32_t)f.prim : G::NONE;
+    L.inst = f.inst;
+    L.nobox = true;
+    Aabb local, ext;
+    bool has_local = false;
+    const bool has_ext = f.prim >= 0 && prim_extent((uint32_t)f.prim, ext);
+    if (f.has_box && !f.ref_only) { local = f.box; has_local = true; }
+    else if (has_ext) { local = f.has_box ? box_union(f.box, ext) : ext; has_local = true; }
+    if (has_local) L.nobox = !(f.inst == G::NONE ? (L.box = local, finite_box(local)) : to_world(local, f.inst, L.box));
+    if (L.nobox) {
+      ok = false;
+      L.box.mn = v3(-inf, -inf, -inf);
+      L.box.mx = v3(inf, inf, inf);
+    }
+    L.has_rbox = has_wbox;
+    L.rbox = wbox;
+    if (f.inst != G::NONE) {
+      L.gflags |= G::GL_INST;
+      bool dir = false;
+      for (uint32_t q = f.inst; q != G::NONE; q = s->g_insts[q].parent)
+        dir |= (s->g_insts[q].kind & G::I_KIND_MASK) != G::I_TRANSLATE;
+      if (dir) {
+        L.gflags |= G::GL_DIR;
+        for (uint32_t m = f.begin; m < f.end; m++) {
+          const uint32_t km = (s->g_nodes[m].kp >> 24) & G::KIND_MASK;
+          if (km == G::K_BOX || km == G::K_BOX_PRIM) L.gflags |= G::GL_INV;
+          if ((km == G::K_BOX_PRIM || km == G::K_PRIM) && (s->g_prims[s->g_nodes[m].kp & 0xFFFFFFu].km & 3u) != G::P_RECT)
+            L.gflags |= G::GL_DD;
+        }
+      }
+    }
+    T.push_back(WNode{L.box, (int32_t)leaves.size(), ref_end, (uint32_t)open.size()});
+    start.push_back(f.begin);
+    leaves.push_back(L);
+  };
+  const char* flat_env = getenv("HRT_GWALK_FLAT"); /* "0": instance chains stay whole leaf programs (A/B) */
+  const bool flat_ok = !(flat_env && strcmp(flat_env, "0") == 0);
   uint32_t i = 0;
   while (i < n) {
     while (!open.empty() && open.back().end <= i) open.pop_back();
@@ -978,6 +1116,15 @@ std::vector<WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<WNode>* ref_t
         continue;
       }
       /* the leaf's single primitive, if the subtree is one world-level prim (for its true extent) */
+      std::vector<Flat> fl;
+      bool chains = false;
+      for (uint32_t j = i + 1; j < skip; j++) chains |= ((s->g_nodes[j].kp >> 24) & G::KIND_MASK) == G::K_INST_BEGIN;
+      if (chains && flat_ok && flatten_chains(i + 1, skip, fl) && !fl.empty()) {
+        /* the BvhNode leaf's box is tested (world frame) before each flattened leaf's program */
+        for (size_t q = 0; q < fl.size(); q++) add_flat(fl[q], true, node_box(i), q + 1 < fl.size() ? fl[q + 1].begin : skip);
+        i = skip;
+        continue;
+      }
       const int prim = (skip == i + 2 && ((s->g_nodes[i + 1].kp >> 24) & G::KIND_MASK) == G::K_PRIM)
                            ? (int)(s->g_nodes[i + 1].kp & 0xFFFFFFu) : -1;
       add_leaf(i, skip, true, node_box(i), ref_only, prim);
@@ -997,6 +1144,14 @@ std::vector<WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<WNode>* ref_t
         else if (k == G::K_INST_END && --depth == 0) break;
       }
       need(j < n, HRT_ERR_STATE, "general walk stream: unbalanced instance brackets");
+      std::vector<Flat> fl;
+      if (flat_ok && flatten_chains(i, j + 1, fl) && !fl.empty()) {
+        const bool wb = !open.empty();
+        const Aabb wbox = wb ? open.back().box : Aabb{};
+        for (size_t q = 0; q < fl.size(); q++) add_flat(fl[q], wb, wbox, q + 1 < fl.size() ? fl[q + 1].begin : j + 1);
+        i = j + 1;
+        continue;
+      }
       add_leaf(i, j + 1, false, Aabb{}, false, -1);
       i = j + 1;
     } else if (kind == G::K_MEDIUM) {

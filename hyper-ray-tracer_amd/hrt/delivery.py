@@ -90,6 +90,12 @@ class FrameDelivery:
             dist.barrier(group=group)
         if rank != 0:
             self.shm = shared_memory.SharedMemory(name=name[0])
+            try:  # rank 0 owns (and unlinks) the segment: keep this process's tracker from unlinking it too
+                from multiprocessing import resource_tracker
+
+                resource_tracker.unregister(self.shm._name, "shared_memory")
+            except Exception:
+                pass
         self.hdr = np.ndarray((HDR_BYTES // 8,), np.int64, self.shm.buf)  # ready[0..world-1], consumed, error
         self.frames = [np.ndarray((height * width, 4), np.float32, self.shm.buf, HDR_BYTES + s * self.frame_bytes)
                        for s in range(2)]

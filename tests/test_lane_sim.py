@@ -203,3 +203,18 @@ def test_general_walk_stream_regrouped_equals_reference_hierarchy(sim, earth, na
     assert sa["segments"] == sb["segments"] and sa["prims"] == sb["prims"]
     assert np.array_equal(a, b)
     print(name, "node visits: re-grouped", sa["nodes"], "reference hierarchy", sb["nodes"])
+
+
+@pytest.mark.parametrize("name", ["cornell", "final", "features"])
+def test_flattened_instance_chains_equal_whole_programs(sim, earth, name, monkeypatch):
+    """Instance chains flattened into leaves of their own (each in the innermost frame, after the
+    world-frame box test around the chain: layout.h GL_INST) against whole-chain leaf programs
+    (HRT_GWALK_FLAT=0): bit-identical, with fewer primitive tests (each flattened leaf is culled by the
+    world image of its own geometry)."""
+    a, sa = sim_render(sim, name, 32, 24, 4, 50, 6, earth, kernel=3, cull=CULL_EXACT)
+    monkeypatch.setenv("HRT_GWALK_FLAT", "0")
+    b, sb = sim_render(sim, name, 32, 24, 4, 50, 6, earth, kernel=3, cull=CULL_EXACT)
+    assert sa["segments"] == sb["segments"]
+    assert np.array_equal(a, b)
+    assert sa["prims"] <= sb["prims"]
+    print(name, "primitive tests: flattened", sa["prims"], "whole programs", sb["prims"])
