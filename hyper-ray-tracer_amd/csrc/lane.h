@@ -1173,7 +1173,7 @@ HRT_LANE_FI void walk_prim(const KParams& P, const WalkSrc& src, uint32_t& i, co
 template <bool MEDIA, bool COUNT, int MEM>
 HRT_LANE_FI void gwalk_leaf_test(const KParams& P, const G::Node* __restrict__ nodes, const G::Prim* __restrict__ prims,
                                  const WalkSrc& src, uint32_t leaf, const TRay& r, float& closest, uint32_t& winner,
-                                 const PathKey& pk, Counts& cn) {
+                                 uint32_t& gstate, const PathKey& pk, Counts& cn) {
   const float4 h = wload<MEM>(src, leaf);
   const uint32_t flags = f2u(h.z);
   if (!(flags & (G::GL_BOX | G::GL_INST))) {
@@ -1181,9 +1181,11 @@ HRT_LANE_FI void gwalk_leaf_test(const KParams& P, const G::Node* __restrict__ n
     return;
   }
   const float4 bmn = wload<MEM>(src, leaf + 16u);
-  if (flags & G::GL_BOX) {
+  if (flags & G::GL_BOX) { /* the group's box: tested at the group's first leaf, the outcome kept (layout.h) */
     const float4 bmx = wload<MEM>(src, leaf + 32u);
-    if (!box_ref(bmn, bmx, r, P.t_min, closest)) return;
+    const uint32_t g = f2u(bmx.w);
+    if ((gstate & 0x7FFFFFFFu) != g) gstate = g | (box_ref(bmn, bmx, r, P.t_min, closest) ? 0x80000000u : 0u);
+    if (!(gstate >> 31)) return;
   }
   if (!(flags & G::GL_INST)) {
     trace_ray<G::CULL_EXACT, true, MEDIA, COUNT>(P, nodes, prims, f2u(h.x), f2u(h.y), r, P.t_min, closest, winner, pk, cn);
@@ -1205,10 +1207,10 @@ HRT_LANE_FI void gwalk_leaf_test(const KParams& P, const G::Node* __restrict__ n
 template <bool MEDIA, bool COUNT, int MEM>
 HRT_LANE_FI void gwalk_prim(const KParams& P, const G::Node* __restrict__ nodes, const G::Prim* __restrict__ prims,
                             const WalkSrc& src, uint32_t& i, const TRay& r, float& closest, uint32_t& winner,
-                            const PathKey& pk, Counts& cn) {
+                            uint32_t& gstate, const PathKey& pk, Counts& cn) {
   const uint32_t leaf = i - WALK_PEND;
   i = walk_successor<MEM>(src, leaf);
-  gwalk_leaf_test<MEDIA, COUNT, MEM>(P, nodes, prims, src, leaf, r, closest, winner, pk, cn);
+  gwalk_leaf_test<MEDIA, COUNT, MEM>(P, nodes, prims, src, leaf, r, closest, winner, gstate, pk, cn);
 }
 
 /* both halves back to back (the host lane simulator's walk) */

@@ -196,8 +196,13 @@ enum : uint32_t { WT_SOLID = 0, WT_CHECKER = 1, WT_GLOBAL = 2 }; /* inline textu
  * trace_ray from the world ray (the leaf's own box node first: the reference test at the leaf).  Leaf
  * payload (GWALK_PAYLOAD_BYTES):
  *   float4(begin, end, flags, w)     w = successor << 2 (walk_successor, as in the sphere stream)
- *   float4(mn.xyz, inst) float4(mx.xyz, 0)   GL_BOX: the nearest enclosing BvhNode box of a box-less leaf
- *                                         (world frame), whose reference test (aabb.rs) precedes the program
+ *   float4(mn.xyz, inst) float4(mx.xyz, group)   GL_BOX: the nearest enclosing BvhNode box of a box-less
+ *                                         leaf (world frame; `group` = that node's reference-stream index).
+ *                                         The reference tests it once, before all the leaves it holds
+ *                                         (List::hit, Translation::hit below one BvhNode leaf), so a lane
+ *                                         tests it at the first of them it reaches and keeps the outcome
+ *                                         for the rest (lane.h gwalk_leaf_test `gstate`): the closest then is
+ *                                         the reference's, since the walk visits leaves in its order
  * Instance chains are flattened: each leaf object inside a Translation / Rotation (a primitive, a Cuboid,
  * a leaf of the instance's own BvhNode) is a leaf of the stream, its box the chain's image of its geometry.
  * The node part's C, E box holds the leaf's geometry (its reference box, or for a transposed ZX rect

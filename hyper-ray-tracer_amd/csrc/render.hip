@@ -525,7 +525,7 @@ KParams scene_params(const hrt_scene* s, const hrt_camera* cam, const hrt_render
    * DESIGN.md section 10) */
   const bool spec = !pl.full && !pl.general && !pl.fast && pl.cull == G::CULL_EXACT;
   kp.postpone = env_knob("HRT_POSTPONE", pl.gwalk ? 44 : (spec ? (s->w_hot ? 44 : 52) : 56));
-  kp.prim_batch = env_knob("HRT_PRIM_BATCH", (spec || pl.gwalk) ? 4 : 8);
+  kp.prim_batch = env_knob("HRT_PRIM_BATCH", pl.gwalk ? 32 : (spec ? 4 : 8)); /* gwalk: r03d sweep, Cornell 4 / 8 / 16 / 32 = 9496 / 9838 / 10271 / 10474 */
   /* a walk visits each node at most once, a medium's boundary subtree at most twice per medium node */
   kp.walk_cap = 3u * (uint32_t)s->g_nodes.size() + 64u;
   kp.motion_uniform = s->motion_uniform ? 1u : 0u;

@@ -88,6 +88,7 @@ void render_gwalk_kernel(KParams P) {
   TRay r;
   set_ray(r, ps.ro, ps.rd, 0.0f, P);
   uint32_t node = G::NONE, winner = G::NONE, pend = G::NONE;
+  uint32_t gstate = G::NONE; /* the last leaf group whose box this walk tested, and its outcome (bit 31) */
   float closest = inf;
   uint32_t n_seg = 0, n_samples = 0, n_pixels = 0;
   Counts cn{0u, 0u, 0u, 0u, 0u, 0u};
@@ -115,6 +116,7 @@ void render_gwalk_kernel(KParams P) {
       set_ray(r, ps.ro, ps.rd, ps.rtime, P);
       closest = inf;
       winner = G::NONE;
+      gstate = G::NONE & 0x7FFFFFFFu;
       node = ps.depth_left == 0 ? G::NONE : 0u; /* max_depth 0: black without a world.hit (:478-480) */
       setup = false;
     }
@@ -145,7 +147,7 @@ void render_gwalk_kernel(KParams P) {
         if (pm && ((uint32_t)__popcll(pm) >= batch || !__ballot(node < end))) {
           if constexpr (COUNT) cn.prim_slots++;
           if (pend != G::NONE) {
-            gwalk_leaf_test<MEDIA, COUNT, WMEM>(P, nodes, prims, ws, pend, r, closest, winner, ps.pk, cn);
+            gwalk_leaf_test<MEDIA, COUNT, WMEM>(P, nodes, prims, ws, pend, r, closest, winner, gstate, ps.pk, cn);
             pend = G::NONE;
             if (walk_pending(node)) {
               pend = node - WALK_PEND;

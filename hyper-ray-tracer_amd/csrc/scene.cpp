@@ -789,15 +789,16 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
       const uint32_t q = paddr[i];
       put4(o, q, u2f(L.begin), u2f(L.end), u2f((L.has_rbox ? G::GL_BOX : 0u) | L.gflags), u2f(skip << 2));
       put4(o, q + 16, L.rbox.mn.x, L.rbox.mn.y, L.rbox.mn.z, u2f(L.inst));
-      put4(o, q + 32, L.rbox.mx.x, L.rbox.mx.y, L.rbox.mx.z, 0.0f);
+      put4(o, q + 32, L.rbox.mx.x, L.rbox.mx.y, L.rbox.mx.z, u2f(L.rgroup));
       continue;
     }
     const G::Prim& p = s->g_prims[L.prim];
     const bool moving = (p.km & 3u) == G::P_MOVING;
     /* the reference test at the leaf: its own box, or for a box-less List member the nearest enclosing
      * BvhNode box (monotone: it implies every enclosing box's test), or none at world level */
-    const bool ref_test = !L.nobox || L.has_rbox;
-    const Aabb& rb = L.nobox ? L.rbox : L.box;
+    const bool ref_test = !L.nobox;
+    need(!L.has_rbox, HRT_ERR_STATE, "sphere walk stream: a leaf needs its group's box test (general stream)");
+    const Aabb& rb = L.box;
     const uint32_t wflags = (moving ? G::WL_MOVING : 0u) | (ref_test ? 0u : G::WL_NOBOX) | (skip << 2);
     const uint32_t q = paddr[i];
     put4(o, q, rb.mn.x, rb.mn.y, rb.mn.z, u2f(wflags));
@@ -863,6 +864,7 @@ std::vector<WalkLeaf> walk_leaves(const hrt_scene* s, std::vector<WNode>* ref_tr
     if (L.nobox && !open.empty()) { /* a List member inside a BvhNode leaf: that box's reference test */
       L.has_rbox = true;
       L.rbox = T[open.back()].box;
+      L.rgroup = open.back();
     }
     for (int k = 0; k < 3 && !L.nobox; k++)
       if (!(g.mn[k] <= g.mx[k]) || !std::isfinite(g.mn[k]) || !std::isfinite(g.mx[k])) ok = false;
@@ -885,7 +887,7 @@ std::vector<WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<WNode>* ref_t
   std::vector<WalkLeaf> leaves;
   std::vector<WNode> T;
   std::vector<uint32_t> start; /* reference-stream index at which each hierarchy node starts */
-  struct Open { uint32_t end; Aabb box; };
+  struct Open { uint32_t end; Aabb box; uint32_t node; };
   std::vector<Open> open;
   bool ok = true;
   auto node_box = [&](uint32_t i) {
@@ -1043,6 +1045,7 @@ std::vector<WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<WNode>* ref_t
     if (!has_box && !open.empty()) { /* box-less: the nearest enclosing BvhNode's reference test first */
       L.has_rbox = true;
       L.rbox = open.back().box;
+      L.rgroup = open.back().node;
     }
     T.push_back(WNode{L.box, (int32_t)leaves.size(), end, (uint32_t)open.size()});
     start.push_back(begin);
@@ -1050,7 +1053,7 @@ std::vector<WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<WNode>* ref_t
   };
   /* a leaf of a flattened chain: its program in the frame of `f.inst`, after the reference test of the
    * world-frame box `wbox` around the chain (if any) */
-  auto add_flat = [&](const Flat& f, bool has_wbox, const Aabb& wbox, uint32_t ref_end) {
+  auto add_flat = [&](const Flat& f, bool has_wbox, const Aabb& wbox, uint32_t wgroup, uint32_t ref_end) {
     WalkLeaf L;
     L.begin = f.begin;
     L.end = f.end;
@@ -1070,6 +1073,7 @@ std::vector<WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<WNode>* ref_t
     }
     L.has_rbox = has_wbox;
     L.rbox = wbox;
+    L.rgroup = wgroup;
     if (f.inst != G::NONE) {
       L.gflags |= G::GL_INST;
       bool dir = false;
@@ -1111,7 +1115,7 @@ std::vector<WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<WNode>* ref_t
       if (hierarchy) {
         T.push_back(WNode{node_box(i), -1, skip, (uint32_t)open.size()});
         start.push_back(i);
-        open.push_back(Open{skip, node_box(i)});
+        open.push_back(Open{skip, node_box(i), i});
         i++;
         continue;
       }
@@ -1121,7 +1125,7 @@ std::vector<WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<WNode>* ref_t
       for (uint32_t j = i + 1; j < skip; j++) chains |= ((s->g_nodes[j].kp >> 24) & G::KIND_MASK) == G::K_INST_BEGIN;
       if (chains && flat_ok && flatten_chains(i + 1, skip, fl) && !fl.empty()) {
         /* the BvhNode leaf's box is tested (world frame) before each flattened leaf's program */
-        for (size_t q = 0; q < fl.size(); q++) add_flat(fl[q], true, node_box(i), q + 1 < fl.size() ? fl[q + 1].begin : skip);
+        for (size_t q = 0; q < fl.size(); q++) add_flat(fl[q], true, node_box(i), i, q + 1 < fl.size() ? fl[q + 1].begin : skip);
         i = skip;
         continue;
       }
@@ -1148,7 +1152,8 @@ std::vector<WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<WNode>* ref_t
       if (flat_ok && flatten_chains(i, j + 1, fl) && !fl.empty()) {
         const bool wb = !open.empty();
         const Aabb wbox = wb ? open.back().box : Aabb{};
-        for (size_t q = 0; q < fl.size(); q++) add_flat(fl[q], wb, wbox, q + 1 < fl.size() ? fl[q + 1].begin : j + 1);
+        const uint32_t wg = wb ? open.back().node : G::NONE;
+        for (size_t q = 0; q < fl.size(); q++) add_flat(fl[q], wb, wbox, wg, q + 1 < fl.size() ? fl[q + 1].begin : j + 1);
         i = j + 1;
         continue;
       }
@@ -1211,6 +1216,22 @@ void build_walk(hrt_scene* s) {
   bool regroup_ok = false;
   const std::vector<WalkLeaf> leaves = walk_leaves(s, &T, &regroup_ok);
   if (leaves.empty()) return;
+  for (const WalkLeaf& L : leaves)
+    if (L.has_rbox) { /* a List member inside a BvhNode leaf: the box is tested once for the whole List,
+                       * which the general stream's group test does (render_gwalk_kernel) */
+      std::vector<WNode> TG;
+      bool gok = false;
+      const std::vector<WalkLeaf> gl = gwalk_leaves(s, &TG, &gok);
+      s->w_general = true;
+      const char* md = getenv("HRT_WALK_TREE");
+      if (gok && !(md && strcmp(md, "reference") == 0)) {
+        TG.clear();
+        walk_regroup(TG, gl);
+        s->w_regrouped = true;
+      }
+      walk_place_and_write(s, TG, gl);
+      return;
+    }
   const char* mode = getenv("HRT_WALK_TREE");
   const char* wb = getenv("HRT_WALK_BUILD"); /* host | device | auto (default) */
   const bool regroup = regroup_ok && !(mode && strcmp(mode, "reference") == 0);

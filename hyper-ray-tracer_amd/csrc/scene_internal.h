@@ -73,6 +73,8 @@ struct WalkLeaf {
   uint32_t begin = 0, end = 0;
   bool has_rbox = false;
   Aabb rbox{};
+  uint32_t rgroup = 0xFFFFFFFFu; /* the BvhNode (reference-stream index) rbox belongs to: the reference
+                                    tests it ONCE before all the leaves it holds (layout.h GL_BOX) */
   uint32_t inst = 0xFFFFFFFFu; /* innermost enclosing instance of a flattened leaf (layout.h GL_INST) */
   uint32_t gflags = 0;         /* layout.h GL_INST | GL_DIR | GL_INV | GL_DD */
 };

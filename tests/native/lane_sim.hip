@@ -55,13 +55,14 @@ void render_pixel(const KParams& P, uint32_t px, uint32_t py, float* rgba, uint6
       for (;;) {
         bool traced, done;
         if constexpr (KIND == 3) { /* render_gwalk_kernel: the general walk stream, leaf programs, shade<true> */
-          uint32_t node = ps.depth_left == 0 ? G::NONE : 0u, winner = G::NONE;
+          uint32_t node = ps.depth_left == 0 ? G::NONE : 0u, winner = G::NONE, gstate = 0x7FFFFFFFu;
           float closest = inf;
           WalkSrc src;
           src.base = P.walk;
           while (node < P.walk_end) {
             walk_box<true, WM_HOST>(src, node, r, P.t_min, closest, cn);
-            if (walk_pending(node)) gwalk_prim<true, true, WM_HOST>(P, P.nodes, P.prims, src, node, r, closest, winner, ps.pk, cn);
+            if (walk_pending(node))
+              gwalk_prim<true, true, WM_HOST>(P, P.nodes, P.prims, src, node, r, closest, winner, gstate, ps.pk, cn);
           }
           traced = node != G::NONE;
           done = true;
@@ -171,7 +172,7 @@ int lane_sim_render(const void* blob, const hrt_blob_info* bi, const hrt_camera*
   P.background = v3(p->background[0], p->background[1], p->background[2]);
   P.seed = p->seed;
   if (kernel == 0 && (bi->feature_mask & ~G::F_BASIC) != 0) return 1; /* not a sphere scene */
-  if (kernel == 3 && ((bi->feature_mask & ~G::F_BASIC) == 0 || bi->walk_bytes == 0)) return 1; /* no general stream */
+  if (kernel == 3 && bi->walk_bytes == 0) return 1; /* no general stream */
   for (uint32_t y = 0; y < h; y++)
     for (uint32_t x = 0; x < w; x++) {
       float* o = rgba + 4 * ((size_t)y * w + x);

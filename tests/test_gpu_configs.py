@@ -85,6 +85,18 @@ def test_c5_cornell_2048_10000spp_bands(earth):
 
 
 @pytest.mark.gpu
+def test_cornell_group_box_pixel(earth):
+    """The C5 pixel where re-testing a flattened instance group's box per leaf lost 12 rays
+    (tests/test_lane_sim.py::test_group_box_is_tested_once_per_group), on the GPU at 10000 spp."""
+    W, H, spp = 2048, 2048, 10000
+    img, st = _gpu_rows("cornell", W, H, spp, [300], earth, 1760, 32)
+    ref, cnt = O.OracleScene(hrt.PRESETS["cornell"], 1, earth).render_rows(W, H, spp, [300], 50, seed=1, threads=THREADS,
+                                                                          x0=1760, w=32, task_w=8)
+    assert st.segments == cnt["segments"]
+    assert float(np.abs(img - ref).max()) <= TOL
+
+
+@pytest.mark.gpu
 def test_device_built_walk_vs_oracle(earth):
     """A scene of 39.9k leaves (random_40k: the Random builder over a 200 x 200 grid) takes the
     device-side build of the walk hierarchy by default (build_walk.hip, >= 32768 leaves); its frame band
