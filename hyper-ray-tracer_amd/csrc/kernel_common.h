@@ -24,7 +24,7 @@ void hip_check(hipError_t e, const char* what);
 /* persistent grid: as many workgroups as are co-resident on the device (cached per kernel/device) */
 int resident_grid(const void* fn, int block, int device, size_t smem, bool lds);
 /* render_sphere.hip: launch render_basic_kernel<cull, count, lds> */
-void launch_sphere(int cull, bool count, bool lds, const lane::KParams& kp, int device, hipStream_t stream,
+void launch_sphere(int cull, bool count, bool lds, bool heavy, const lane::KParams& kp, int device, hipStream_t stream,
                    size_t smem);
 /* render_general.hip: launch render_gwalk_kernel (wmem: lane.h WM_*, lref: reference stream in LDS,
  * trim: lane.h TRIM_* features compiled out) */

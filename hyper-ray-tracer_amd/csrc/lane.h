@@ -80,6 +80,7 @@ struct KParams {
   uint32_t walk_end;   /* byte offset one past the last record */
   uint32_t walk_hot;   /* WM_HYB: offsets below this are staged in LDS (layout.h placement) */
   uint32_t lane_lds;   /* sphere kernel: LDS byte offset of the per-lane result slots (after the staged scene) */
+  uint32_t n_insts, n_media, n_mats, n_texs; /* record counts (render_gwalk_kernel stages them in LDS) */
 };
 
 /* Sample-chunk size: spp <= cmin keeps one work item per pixel (the reference's sequential sum), larger
@@ -915,7 +916,10 @@ HRT_LANE_FI bool shade(const KParams& P, PathState& ps, uint32_t winner, float c
 
 /* shade() for the sphere kernel's walk stream: the winner is a leaf record (layout.h), which holds the
  * sphere and its material, so the hit record and the scatter read the walk stream only (LDS). */
-template <bool COUNT, int MEM>
+/* HEAVY: the scene also has noise / image textures (read from texs through the material, WT_GLOBAL):
+ * Perlin turbulence and the image lookup with the sphere's (u, v) are out-of-line calls (tex_heavy,
+ * sphere_uv), made only by lanes whose material needs them. */
+template <bool COUNT, int MEM, bool HEAVY = false>
 HRT_LANE_FI bool shade_walk(const KParams& P, const WalkSrc& src, PathState& ps, uint32_t leaf, float closest,
                             Vec3 ro, Vec3 rd, float rtime, float tau, Vec3& sum, Counts& cn) {
   if (leaf == G::NONE) { /* a sphere scene's path gathers radiance at its miss only: straight into the sum
@@ -952,6 +956,11 @@ HRT_LANE_FI bool shade_walk(const KParams& P, const WalkSrc& src, PathState& ps,
       if constexpr (COUNT) cn.tex += 2;
       return checker_odd(10.0f * rec.p.x, 10.0f * rec.p.y, 10.0f * rec.p.z) ? v3(ma.x, ma.y, ma.z)
                                                                              : v3(mb.x, mb.y, mb.z);
+    }
+    if constexpr (HEAVY) { /* sphere.rs:31-35 (u, v) only under an image texture (Mat.needs_uv) */
+      const G::Mat& M = P.mats[rec.mat];
+      if (M.needs_uv) sphere_uv(outward, rec.u, rec.v);
+      return tex_value<true, COUNT>(P, M.tex, rec.u, rec.v, rec.p, cn);
     }
     return tex_value<false, COUNT>(P, P.mats[rec.mat].tex, rec.u, rec.v, rec.p, cn);
   });

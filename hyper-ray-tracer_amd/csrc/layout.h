@@ -128,6 +128,9 @@ enum : uint32_t {
 };
 /* what the lean kernel instantiation handles (the BASELINE headline scene needs only these) */
 constexpr uint32_t F_BASIC = F_MOVING | F_CHECKER | F_METAL | F_DIELECTRIC;
+/* what the sphere kernel's HEAVY instantiation adds under exact culling: noise and image textures on
+ * sphere scenes (BASELINE config 3, Earth + Perlin) */
+constexpr uint32_t F_HEAVY_TEX = F_NOISE | F_IMAGE;
 
 /* box-culling modes */
 enum : int {

@@ -351,6 +351,7 @@ constexpr size_t LDS_GEN_MAX = 48 * 1024;
 
 struct Plan {
   bool full, fast, lds;
+  bool heavy;    /* sphere scene with noise / image textures on the sphere kernel (HEAVY instantiation) */
   bool gwalk;    /* general scene on render_gwalk_kernel (the general walk stream, render_general.hip) */
   int gwalk_mem; /* its walk-stream placement: WM_LDS / WM_HYB / WM_BUF */
   bool gwalk_lref; /* ... with the reference stream and primitives staged in LDS too */
@@ -364,6 +365,7 @@ struct Plan {
 Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
   Plan pl;
   pl.full = (s->feature_mask & ~G::F_BASIC) != 0;
+  pl.heavy = false;
   /* default: exact.  A ray time outside the interval the BVH boxes were built for can put a moving
    * sphere outside its box: only the reference test is then faithful. */
   const bool shutter_ok = cam->time0 >= s->box_t0 && cam->time1 <= s->box_t1;
@@ -395,6 +397,17 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
   /* instantiated: all features (0), no noise / image textures (HEAVY_TEX: Cornell-smoke 124 VGPRs, no
    * spills, +1.9%), neither those nor media (Cornell: 92 VGPRs, 5 waves/SIMD, +19%).  Trimming the
    * medium branch alone measured -0.6 / -1% (Earth+Perlin, simple-light), so it is not built. */
+  /* sphere scenes with noise / image textures (Earth + Perlin) under exact culling: the sphere kernel's
+   * HEAVY instantiation over the sphere walk stream (HRT_KERNEL=segment keeps the segment kernel) */
+  const bool seg = k && strcmp(k, "segment") == 0;
+  if (pl.full && (s->feature_mask & ~(G::F_BASIC | G::F_HEAVY_TEX)) == 0 && pl.cull == G::CULL_EXACT && !s->w_general &&
+      s->w_end > 0 && !seg && !(k && strcmp(k, "general") == 0) && !(k && strcmp(k, "persistent") == 0)) {
+    pl.full = false;
+    pl.heavy = true;
+    pl.general = false;
+    pl.smem = s->w_hot ? s->w_hot : s->w_end;
+    pl.lds = (flags & HRT_RENDER_NO_LDS) == 0 && pl.smem <= LDS_SCENE_MAX;
+  }
   pl.trim = 0;
   if ((s->feature_mask & (G::F_NOISE | G::F_IMAGE)) == 0)
     pl.trim = TRIM_HEAVY_TEX | ((s->feature_mask & G::F_MEDIUM) == 0 && !s->media_nested ? TRIM_MEDIA : 0);
@@ -408,7 +421,10 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
   if (pl.gwalk) {
     pl.general = false;
     const size_t walk = s->w_hot ? s->w_hot : s->w_end;
-    const size_t ref = s->g_nodes.size() * sizeof(G::Node) + s->g_prims.size() * sizeof(G::Prim);
+    /* everything leaf programs and shading read, but the Perlin tables and images */
+    const size_t ref = s->g_nodes.size() * sizeof(G::Node) + s->g_prims.size() * sizeof(G::Prim) +
+                       s->g_insts.size() * sizeof(G::Inst) + s->g_media.size() * sizeof(G::Medium) +
+                       s->g_mats.size() * sizeof(G::Mat) + s->g_texs.size() * sizeof(G::Tex);
     const bool no_lds = (flags & HRT_RENDER_NO_LDS) != 0;
     pl.gwalk_mem = no_lds || walk > LDS_SCENE_MAX ? WM_BUF : (s->w_hot ? WM_HYB : WM_LDS);
     const char* lr = getenv("HRT_GWALK_LREF"); /* A/B knob: "0" keeps the reference stream in global memory */
@@ -462,15 +478,15 @@ void launch_any(const hrt_scene* s, const Plan& pl, const KParams& kp, hipStream
   } else if (pl.cull == G::CULL_EXACT) {
     if (pl.full) pl.lds ? launch_full<G::CULL_EXACT, COUNT, true>(kp, s->device, stream, smem)
                         : launch_full<G::CULL_EXACT, COUNT, false>(kp, s->device, stream, 0);
-    else launch_sphere(G::CULL_EXACT, COUNT, pl.lds, kp, s->device, stream, smem);
+    else launch_sphere(G::CULL_EXACT, COUNT, pl.lds, pl.heavy, kp, s->device, stream, smem);
   } else if (pl.cull == G::CULL_SLAB) {
     if (pl.full) pl.lds ? launch_full<G::CULL_SLAB, COUNT, true>(kp, s->device, stream, smem)
                         : launch_full<G::CULL_SLAB, COUNT, false>(kp, s->device, stream, 0);
-    else launch_sphere(G::CULL_SLAB, COUNT, pl.lds, kp, s->device, stream, smem);
+    else launch_sphere(G::CULL_SLAB, COUNT, pl.lds, false, kp, s->device, stream, smem);
   } else {
     if (pl.full) pl.lds ? launch_full<G::CULL_REFERENCE, COUNT, true>(kp, s->device, stream, smem)
                         : launch_full<G::CULL_REFERENCE, COUNT, false>(kp, s->device, stream, 0);
-    else launch_sphere(G::CULL_REFERENCE, COUNT, pl.lds, kp, s->device, stream, smem);
+    else launch_sphere(G::CULL_REFERENCE, COUNT, pl.lds, false, kp, s->device, stream, smem);
   }
 }
 
@@ -518,6 +534,10 @@ KParams scene_params(const hrt_scene* s, const hrt_camera* cam, const hrt_render
   kp.seed = p->seed;
   kp.n_nodes = pl.fast ? 8 * s->f_stream_len : (uint32_t)s->g_nodes.size(); /* main stream + medium boundary subtrees */
   kp.n_prims = (uint32_t)(pl.fast ? s->f_prims.size() : s->g_prims.size());
+  kp.n_insts = (uint32_t)s->g_insts.size();
+  kp.n_media = (uint32_t)s->g_media.size();
+  kp.n_mats = (uint32_t)s->g_mats.size();
+  kp.n_texs = (uint32_t)s->g_texs.size();
   kp.stream_len = pl.fast ? s->f_stream_len : 0;
   /* the sphere kernel's speculative walk (render_sphere.hip SPEC) blocks lanes less often: it runs best
    * with smaller batches; deep streams (top levels in LDS, w_hot: long walks) shade earlier (r02z sweep
@@ -1003,7 +1023,7 @@ hrt_status hrt_debug_trace_path(hrt_scene* s, const hrt_camera* cam, const hrt_r
     hip_check(hipMalloc((void**)&d_out, bytes), "hipMalloc");
     hip_check(hipMalloc((void**)&d_n, 4), "hipMalloc");
     if (pl.fast) hipLaunchKernelGGL((debug_path_kernel<G::CULL_SLAB, false, true>), dim3(1), dim3(64), 0, 0, kp, x, y, sample, d_out, max_segments, d_n);
-    else if (pl.full && pl.cull == G::CULL_EXACT) hipLaunchKernelGGL((debug_path_kernel<G::CULL_EXACT, true, false>), dim3(1), dim3(64), 0, 0, kp, x, y, sample, d_out, max_segments, d_n);
+    else if ((pl.full || pl.heavy) && pl.cull == G::CULL_EXACT) hipLaunchKernelGGL((debug_path_kernel<G::CULL_EXACT, true, false>), dim3(1), dim3(64), 0, 0, kp, x, y, sample, d_out, max_segments, d_n);
     else if (pl.cull == G::CULL_EXACT) hipLaunchKernelGGL((debug_path_kernel<G::CULL_EXACT, false, false>), dim3(1), dim3(64), 0, 0, kp, x, y, sample, d_out, max_segments, d_n);
     else if (pl.full && pl.cull == G::CULL_SLAB) hipLaunchKernelGGL((debug_path_kernel<G::CULL_SLAB, true, false>), dim3(1), dim3(64), 0, 0, kp, x, y, sample, d_out, max_segments, d_n);
     else if (pl.full) hipLaunchKernelGGL((debug_path_kernel<G::CULL_REFERENCE, true, false>), dim3(1), dim3(64), 0, 0, kp, x, y, sample, d_out, max_segments, d_n);

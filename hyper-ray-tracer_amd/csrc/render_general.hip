@@ -53,15 +53,30 @@ void render_gwalk_kernel(KParams P) {
     const float4* g = reinterpret_cast<const float4*>(P.walk);
     for (uint32_t k = threadIdx.x; k < staged / 16u; k += blockDim.x) lds_scene[k] = g[k];
   }
-  if constexpr (LREF) { /* the reference stream and primitives behind it (16-B aligned: the stream is) */
-    const uint32_t n4 = P.n_nodes * (uint32_t)(sizeof(G::Node) / 16), p4 = P.n_prims * (uint32_t)(sizeof(G::Prim) / 16);
+  /* Q: the parameters leaf programs and shading read the scene through.  LREF: every record they read
+   * but the Perlin tables and images (reference stream, primitives, instances, media, materials,
+   * textures) staged in LDS behind the walk stream (all 16-B records), so a leaf's instance chain and a
+   * hit record's node -> primitive -> instance -> material -> texture reads are LDS reads instead of
+   * dependent global loads */
+  KParams Q = P;
+  if constexpr (LREF) {
     float4* dst = lds_scene + staged / 16u;
-    const float4* gn = reinterpret_cast<const float4*>(P.nodes);
-    const float4* gp = reinterpret_cast<const float4*>(P.prims);
-    for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) dst[k] = gn[k];
-    for (uint32_t k = threadIdx.x; k < p4; k += blockDim.x) dst[n4 + k] = gp[k];
-    nodes = reinterpret_cast<const G::Node*>(dst);
-    prims = reinterpret_cast<const G::Prim*>(dst + n4);
+    auto stage = [&](const void* src, uint32_t records, uint32_t bytes) {
+      float4* at = dst;
+      const float4* g = reinterpret_cast<const float4*>(src);
+      const uint32_t n4 = records * (bytes / 16u);
+      for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) at[k] = g[k];
+      dst += n4;
+      return (const void*)at;
+    };
+    Q.nodes = static_cast<const G::Node*>(stage(P.nodes, P.n_nodes, sizeof(G::Node)));
+    Q.prims = static_cast<const G::Prim*>(stage(P.prims, P.n_prims, sizeof(G::Prim)));
+    Q.insts = static_cast<const G::Inst*>(stage(P.insts, P.n_insts, sizeof(G::Inst)));
+    Q.media = static_cast<const G::Medium*>(stage(P.media, P.n_media, sizeof(G::Medium)));
+    Q.mats = static_cast<const G::Mat*>(stage(P.mats, P.n_mats, sizeof(G::Mat)));
+    Q.texs = static_cast<const G::Tex*>(stage(P.texs, P.n_texs, sizeof(G::Tex)));
+    nodes = Q.nodes;
+    prims = Q.prims;
   }
   __syncthreads();
   if ((WMEM == WM_LDS || WMEM == WM_HYB) && lds_base != 0u) { /* stream offsets are LDS addresses */
@@ -126,16 +141,19 @@ void render_gwalk_kernel(KParams P) {
     uint32_t iters = 0;
     bool stuck = false;
     for (;;) {
+      /* the node steps unrolled on their own, the leaf block after every PRIM_EVERY of them: unrolling
+       * the block with them made the loop too large for the unroller */
+      for (int v = 0; v < WALK_UNROLL / PRIM_EVERY; v++) {
 #pragma unroll
-      for (int u = 0; u < WALK_UNROLL; u++) {
-        if constexpr (COUNT) cn.walk_slots++;
-        if (node < end) {
-          walk_box<COUNT, WMEM>(ws, node, r, tmin_c, closest, cn);
-        } else if constexpr (COUNT) {
-          if (walk_pending(node)) cn.park_slots++;
-          else if (walking) cn.wait_slots++;
+        for (int u = 0; u < PRIM_EVERY; u++) {
+          if constexpr (COUNT) cn.walk_slots++;
+          if (node < end) {
+            walk_box<COUNT, WMEM>(ws, node, r, tmin_c, closest, cn);
+          } else if constexpr (COUNT) {
+            if (walk_pending(node)) cn.park_slots++;
+            else if (walking) cn.wait_slots++;
+          }
         }
-        if ((u + 1) % PRIM_EVERY != 0) continue;
         /* speculative walk (render_sphere.hip): a passed leaf's program waits in `pend` while the lane
          * walks on; the wave runs the pending programs once `batch` lanes are blocked or none can step */
         if (walk_pending(node) && pend == G::NONE) {
@@ -147,7 +165,7 @@ void render_gwalk_kernel(KParams P) {
         if (pm && ((uint32_t)__popcll(pm) >= batch || !__ballot(node < end))) {
           if constexpr (COUNT) cn.prim_slots++;
           if (pend != G::NONE) {
-            gwalk_leaf_test<MEDIA, COUNT, WMEM>(P, nodes, prims, ws, pend, r, closest, winner, gstate, ps.pk, cn);
+            gwalk_leaf_test<MEDIA, COUNT, WMEM>(Q, nodes, prims, ws, pend, r, closest, winner, gstate, ps.pk, cn);
             pend = G::NONE;
             if (walk_pending(node)) {
               pend = node - WALK_PEND;
@@ -177,7 +195,7 @@ void render_gwalk_kernel(KParams P) {
       bool done = true;
       if (traced) {
         ps.pk.segment++;
-        done = shade<true, COUNT, TRIM>(P, ps, winner, closest, r.o, r.d, r.time, r.tau, cn) || ps.depth_left == 0;
+        done = shade<true, COUNT, TRIM>(Q, ps, winner, closest, r.o, r.d, r.time, r.tau, cn) || ps.depth_left == 0;
       }
       if (done) {
         walking = false;

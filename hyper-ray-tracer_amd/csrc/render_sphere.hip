@@ -18,7 +18,7 @@ namespace {
 
 /* HYB (CULL_EXACT with LDS): the walk stream exceeds the LDS budget; its first P.walk_hot bytes (the
  * hierarchy's top levels) are staged, the rest is read through the buffer descriptor (layout.h) */
-template <int CULL, bool COUNT, bool LDS, bool HYB = false>
+template <int CULL, bool COUNT, bool LDS, bool HYB = false, bool HEAVY = false>
 __global__ __launch_bounds__(basic_block_threads<LDS>(), BASIC_WAVES)
 void render_basic_kernel(KParams P) {
   extern __shared__ float4 lds_scene[];
@@ -185,7 +185,7 @@ void render_basic_kernel(KParams P) {
     if (shading) {
       bool done = true;
       if (traced) {
-        if constexpr (WS) done = shade_walk<COUNT, WMEM>(P, ws, ps, winner, closest, r.o, r.d, r.time, r.tau, sum, cn);
+        if constexpr (WS) done = shade_walk<COUNT, WMEM, HEAVY>(P, ws, ps, winner, closest, r.o, r.d, r.time, r.tau, sum, cn);
         else done = shade<false, COUNT>(P, ps, winner, closest, r.o, r.d, r.time, r.tau, cn);
         done = done || ps.depth_left == 0;
       }
@@ -227,9 +227,9 @@ void render_basic_kernel(KParams P) {
 }
 
 
-template <int CULL, bool COUNT, bool LDS, bool HYB = false>
+template <int CULL, bool COUNT, bool LDS, bool HYB = false, bool HEAVY = false>
 void launch_basic(const KParams& kp, int device, hipStream_t stream, size_t smem) {
-  const void* fn = (const void*)render_basic_kernel<CULL, COUNT, LDS, HYB>;
+  const void* fn = (const void*)render_basic_kernel<CULL, COUNT, LDS, HYB, HEAVY>;
   const int block = basic_block_threads<LDS>();
   /* LDS: the staged scene, then one u32 result slot per thread (layout.h LDS_SCENE_MAX_BYTES leaves
    * room for both, twice per CU) */
@@ -237,7 +237,7 @@ void launch_basic(const KParams& kp, int device, hipStream_t stream, size_t smem
   p.lane_lds = LDS ? (uint32_t)((smem + 15) & ~(size_t)15) : 0u;
   const size_t total = p.lane_lds + (size_t)block * sizeof(uint32_t);
   const int grid = resident_grid(fn, block, device, total, true);
-  hipLaunchKernelGGL((render_basic_kernel<CULL, COUNT, LDS, HYB>), dim3(grid), dim3(block), total, stream, p);
+  hipLaunchKernelGGL((render_basic_kernel<CULL, COUNT, LDS, HYB, HEAVY>), dim3(grid), dim3(block), total, stream, p);
   hip_check(hipGetLastError(), "render_basic_kernel launch");
 }
 
@@ -246,7 +246,15 @@ void launch_basic(const KParams& kp, int device, hipStream_t stream, size_t smem
 
 namespace hrt {
 
-void launch_sphere(int cull, bool count, bool lds, const KParams& kp, int device, hipStream_t stream, size_t smem) {
+void launch_sphere(int cull, bool count, bool lds, bool heavy, const KParams& kp, int device, hipStream_t stream,
+                   size_t smem) {
+  if (heavy) { /* noise / image textures (exact culling only: plan()) */
+    if (count) lds ? launch_basic<G::CULL_EXACT, true, true, false, true>(kp, device, stream, smem)
+                   : launch_basic<G::CULL_EXACT, true, false, false, true>(kp, device, stream, 0);
+    else lds ? launch_basic<G::CULL_EXACT, false, true, false, true>(kp, device, stream, smem)
+             : launch_basic<G::CULL_EXACT, false, false, false, true>(kp, device, stream, 0);
+    return;
+  }
   if (cull == G::CULL_EXACT && lds && kp.walk_hot > 0) { /* top levels in LDS, the rest in global memory */
     if (count) launch_basic<G::CULL_EXACT, true, true, true>(kp, device, stream, smem);
     else launch_basic<G::CULL_EXACT, false, true, true>(kp, device, stream, smem);

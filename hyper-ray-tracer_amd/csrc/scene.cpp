@@ -1193,7 +1193,7 @@ void build_walk(hrt_scene* s) {
   s->w_device_built = false;
   s->w_regroup_pending = false;
   s->w_general = false;
-  if ((s->feature_mask & ~G::F_BASIC) != 0) { /* general scenes: the leaf-object stream (layout.h) */
+  if ((s->feature_mask & ~(G::F_BASIC | G::F_HEAVY_TEX)) != 0) { /* general scenes: the leaf-object stream */
     const char* gw = getenv("HRT_GWALK"); /* "0": no general walk stream (segment kernels only) */
     if ((gw && strcmp(gw, "0") == 0) || s->media_nested) return;
     std::vector<WNode> T;
@@ -1702,6 +1702,7 @@ hrt_status hrt_debug_scene_blob(hrt_scene* s, void* out, uint64_t cap, uint64_t*
       info->walk_regrouped = s->w_regrouped ? 1u : 0u;
       info->bvh_tied_sorts = s->bvh_tied_sorts;
       info->walk_hot = s->w_hot;
+      info->walk_general = s->w_general ? 1u : 0u;
     }
   });
 }

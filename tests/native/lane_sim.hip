@@ -94,7 +94,7 @@ void render_pixel(const KParams& P, uint32_t px, uint32_t py, float* rgba, uint6
           if constexpr (CULL == G::CULL_EXACT) {
             WalkSrc src;
             src.base = P.walk;
-            done = !traced || shade_walk<true, WM_HOST>(P, src, ps, winner, closest, r.o, r.d, r.time, r.tau, sum, cn) ||
+            done = !traced || shade_walk<true, WM_HOST, true>(P, src, ps, winner, closest, r.o, r.d, r.time, r.tau, sum, cn) ||
                    ps.depth_left == 0;
           } else {
             done = !traced ||
@@ -171,8 +171,9 @@ int lane_sim_render(const void* blob, const hrt_blob_info* bi, const hrt_camera*
   P.t_min = p->t_min;
   P.background = v3(p->background[0], p->background[1], p->background[2]);
   P.seed = p->seed;
-  if (kernel == 0 && (bi->feature_mask & ~G::F_BASIC) != 0) return 1; /* not a sphere scene */
-  if (kernel == 3 && bi->walk_bytes == 0) return 1; /* no general stream */
+  if (kernel == 0 && (bi->feature_mask & ~(G::F_BASIC | G::F_HEAVY_TEX)) != 0) return 1; /* not a sphere scene */
+  if (kernel == 3 && (bi->walk_bytes == 0 || !bi->walk_general)) return 1; /* no general stream */
+  if (kernel == 0 && bi->walk_general && cull == G::CULL_EXACT) return 1;      /* no sphere stream */
   for (uint32_t y = 0; y < h; y++)
     for (uint32_t x = 0; x < w; x++) {
       float* o = rgba + 4 * ((size_t)y * w + x);

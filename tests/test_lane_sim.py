@@ -28,6 +28,8 @@ ROOT = os.path.dirname(HERE)
 TOL = 1e-3
 CULL_REFERENCE, CULL_SLAB, CULL_EXACT = 0, 1, 2
 BASIC_SCENES = {"random", "two_spheres", "random_10k"}
+# sphere scenes with noise / image textures: the sphere kernel's HEAVY instantiation (layout.h F_HEAVY_TEX)
+HEAVY_SPHERE_SCENES = {"earth", "two_perlin_spheres", "earth_perlin"}
 
 
 @pytest.fixture(scope="module")
@@ -100,7 +102,7 @@ def test_segment_kernel_lane_matches_general_kernel_lane(sim, earth, name, w, h,
     assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("name,w,h,spp,depth", [c for c in CASES if c[0] in BASIC_SCENES])
+@pytest.mark.parametrize("name,w,h,spp,depth", [c for c in CASES if c[0] in BASIC_SCENES | HEAVY_SPHERE_SCENES])
 def test_sphere_kernel_lane_matches_oracle_and_general_kernel(sim, earth, name, w, h, spp, depth):
     img, st = sim_render(sim, name, w, h, spp, depth, 3, earth, kernel=0, cull=CULL_EXACT)
     ref, cnt = oracle_render(name, w, h, spp, depth, 3, earth)
@@ -178,7 +180,7 @@ def test_walk_stream_regrouped_equals_reference_hierarchy(sim, earth, name, monk
     print(name, "node visits: re-grouped", sa["nodes"], "reference hierarchy", sb["nodes"])
 
 
-GENERAL_CASES = [c for c in CASES if c[0] not in BASIC_SCENES]
+GENERAL_CASES = [c for c in CASES if c[0] not in BASIC_SCENES | HEAVY_SPHERE_SCENES]
 
 
 @pytest.mark.parametrize("name,w,h,spp,depth", GENERAL_CASES)
