@@ -81,6 +81,8 @@ struct KParams {
   uint32_t walk_hot;   /* WM_HYB: offsets below this are staged in LDS (layout.h placement) */
   uint32_t lane_lds;   /* sphere kernel: LDS byte offset of the per-lane result slots (after the staged scene) */
   uint32_t n_insts, n_media, n_mats, n_texs; /* record counts (render_gwalk_kernel stages them in LDS) */
+  uint32_t n_perlin;   /* Perlin tables (7 KB each); perlin_lds: the kernel stages them in LDS */
+  uint32_t perlin_lds;
 };
 
 /* Sample-chunk size: spp <= cmin keeps one work item per pixel (the reference's sequential sum), larger
@@ -722,8 +724,11 @@ HRT_LANE_FI bool checker_odd(float vx, float vy, float vz) {
 
 /* textures/.rs value() */
 HRT_LANE Vec3 tex_heavy(const KParams& P, const G::Tex& T, float u, float v, Vec3 p);
+HRT_LANE_FI Vec3 tex_heavy_inl(const KParams& P, const G::Tex& T, float u, float v, Vec3 p);
 
-template <bool FULL, bool COUNT>
+/* INL: noise / image textures inline (a kernel with the registers to spare: a call saves and restores
+ * the caller's live registers through scratch) instead of the out-of-line tex_heavy */
+template <bool FULL, bool COUNT, bool INL = false>
 HRT_LANE Vec3 tex_value(const KParams& P, uint32_t id, float u, float v, Vec3 p, Counts& cn) {
   for (int guard = 0; guard < 64; guard++) {
     const G::Tex& T = P.texs[id];
@@ -733,6 +738,7 @@ HRT_LANE Vec3 tex_value(const KParams& P, uint32_t id, float u, float v, Vec3 p,
       id = checker_odd(10.0f * p.x, 10.0f * p.y, 10.0f * p.z) ? T.i0 : T.i1;
       continue;
     }
+    if constexpr (FULL && INL) return tex_heavy_inl(P, T, u, v, p);
     if constexpr (FULL) return tex_heavy(P, T, u, v, p);
     break;
   }
@@ -741,7 +747,9 @@ HRT_LANE Vec3 tex_value(const KParams& P, uint32_t id, float u, float v, Vec3 p,
 
 /* Noise and image textures (a solid/checker chain ends in tex_value): out of line, so their
  * registers do not count towards the kernels' walk loops. */
-HRT_LANE_NI Vec3 tex_heavy(const KParams& P, const G::Tex& T, float u, float v, Vec3 p) {
+HRT_LANE_NI Vec3 tex_heavy(const KParams& P, const G::Tex& T, float u, float v, Vec3 p) { return tex_heavy_inl(P, T, u, v, p); }
+
+HRT_LANE_FI Vec3 tex_heavy_inl(const KParams& P, const G::Tex& T, float u, float v, Vec3 p) {
   {
     {
       if (T.kind == G::T_NOISE) { /* noise_texture.rs:24-31 + turbulence perlin_noise.rs:66-78 */
@@ -916,6 +924,9 @@ HRT_LANE_FI bool shade(const KParams& P, PathState& ps, uint32_t winner, float c
 
 /* shade() for the sphere kernel's walk stream: the winner is a leaf record (layout.h), which holds the
  * sphere and its material, so the hit record and the scatter read the walk stream only (LDS). */
+#ifndef HRT_HEAVY_INLINE
+#define HRT_HEAVY_INLINE 0 /* 1: the HEAVY instantiation evaluates textures inline (r03i A/B on C3: 16491 vs 17085 Mrays/s out of line) */
+#endif
 /* HEAVY: the scene also has noise / image textures (read from texs through the material, WT_GLOBAL):
  * Perlin turbulence and the image lookup with the sphere's (u, v) are out-of-line calls (tex_heavy,
  * sphere_uv), made only by lanes whose material needs them. */
@@ -960,7 +971,7 @@ HRT_LANE_FI bool shade_walk(const KParams& P, const WalkSrc& src, PathState& ps,
     if constexpr (HEAVY) { /* sphere.rs:31-35 (u, v) only under an image texture (Mat.needs_uv) */
       const G::Mat& M = P.mats[rec.mat];
       if (M.needs_uv) sphere_uv(outward, rec.u, rec.v);
-      return tex_value<true, COUNT>(P, M.tex, rec.u, rec.v, rec.p, cn);
+      return tex_value<true, COUNT, HRT_HEAVY_INLINE != 0>(P, M.tex, rec.u, rec.v, rec.p, cn);
     }
     return tex_value<false, COUNT>(P, P.mats[rec.mat].tex, rec.u, rec.v, rec.p, cn);
   });

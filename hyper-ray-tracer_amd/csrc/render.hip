@@ -352,6 +352,7 @@ constexpr size_t LDS_GEN_MAX = 48 * 1024;
 struct Plan {
   bool full, fast, lds;
   bool heavy;    /* sphere scene with noise / image textures on the sphere kernel (HEAVY instantiation) */
+  bool perlin_lds; /* the Perlin tables staged in LDS (sphere HEAVY and gwalk kernels) */
   bool gwalk;    /* general scene on render_gwalk_kernel (the general walk stream, render_general.hip) */
   int gwalk_mem; /* its walk-stream placement: WM_LDS / WM_HYB / WM_BUF */
   bool gwalk_lref; /* ... with the reference stream and primitives staged in LDS too */
@@ -366,6 +367,7 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
   Plan pl;
   pl.full = (s->feature_mask & ~G::F_BASIC) != 0;
   pl.heavy = false;
+  pl.perlin_lds = false;
   /* default: exact.  A ray time outside the interval the BVH boxes were built for can put a moving
    * sphere outside its box: only the reference test is then faithful. */
   const bool shutter_ok = cam->time0 >= s->box_t0 && cam->time1 <= s->box_t1;
@@ -407,6 +409,10 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
     pl.general = false;
     pl.smem = s->w_hot ? s->w_hot : s->w_end;
     pl.lds = (flags & HRT_RENDER_NO_LDS) == 0 && pl.smem <= LDS_SCENE_MAX;
+    const size_t perlin = s->perlin.size() * sizeof(G::Perlin);
+    const char* pe = getenv("HRT_PERLIN_LDS"); /* A/B knob: "0" keeps the Perlin tables in global memory */
+    pl.perlin_lds = pl.lds && perlin > 0 && pl.smem + perlin <= LDS_SCENE_MAX && !(pe && strcmp(pe, "0") == 0);
+    if (pl.perlin_lds) pl.smem += perlin;
   }
   pl.trim = 0;
   if ((s->feature_mask & (G::F_NOISE | G::F_IMAGE)) == 0)
@@ -430,6 +436,10 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
     const char* lr = getenv("HRT_GWALK_LREF"); /* A/B knob: "0" keeps the reference stream in global memory */
     pl.gwalk_lref = pl.gwalk_mem == WM_LDS && walk + ref <= LDS_SCENE_MAX && !(lr && strcmp(lr, "0") == 0);
     pl.smem = pl.gwalk_mem == WM_BUF ? 0 : walk + (pl.gwalk_lref ? ref : 0);
+    const size_t perlin = s->perlin.size() * sizeof(G::Perlin);
+    const char* pe = getenv("HRT_PERLIN_LDS");
+    pl.perlin_lds = pl.gwalk_lref && perlin > 0 && pl.smem + perlin <= LDS_SCENE_MAX && !(pe && strcmp(pe, "0") == 0);
+    if (pl.perlin_lds) pl.smem += perlin;
     pl.lds = pl.gwalk_mem != WM_BUF;
     pl.trim = ((s->feature_mask & (G::F_NOISE | G::F_IMAGE)) == 0 ? TRIM_HEAVY_TEX : 0) |
               ((s->feature_mask & G::F_MEDIUM) == 0 ? TRIM_MEDIA : 0);
@@ -538,6 +548,8 @@ KParams scene_params(const hrt_scene* s, const hrt_camera* cam, const hrt_render
   kp.n_media = (uint32_t)s->g_media.size();
   kp.n_mats = (uint32_t)s->g_mats.size();
   kp.n_texs = (uint32_t)s->g_texs.size();
+  kp.n_perlin = (uint32_t)s->perlin.size();
+  kp.perlin_lds = pl.perlin_lds ? 1u : 0u;
   kp.stream_len = pl.fast ? s->f_stream_len : 0;
   /* the sphere kernel's speculative walk (render_sphere.hip SPEC) blocks lanes less often: it runs best
    * with smaller batches; deep streams (top levels in LDS, w_hot: long walks) shade earlier (r02z sweep

@@ -14,12 +14,19 @@ using namespace hrt::kern;
 #define HRT_SPEC 1 /* speculative walk of the walk stream (0: lanes park on every passed leaf, for A/B) */
 #endif
 
+#ifndef HRT_HEAVY_WAVES
+#define HRT_HEAVY_WAVES 4 /* HEAVY: the out-of-line texture calls spill live registers at 80 VGPRs (6 waves) */
+#endif
+
 namespace {
+
+template <bool HEAVY>
+constexpr int sphere_waves() { return HEAVY ? HRT_HEAVY_WAVES : BASIC_WAVES; }
 
 /* HYB (CULL_EXACT with LDS): the walk stream exceeds the LDS budget; its first P.walk_hot bytes (the
  * hierarchy's top levels) are staged, the rest is read through the buffer descriptor (layout.h) */
 template <int CULL, bool COUNT, bool LDS, bool HYB = false, bool HEAVY = false>
-__global__ __launch_bounds__(basic_block_threads<LDS>(), BASIC_WAVES)
+__global__ __launch_bounds__((basic_block_threads<LDS, sphere_waves<HEAVY>()>()), sphere_waves<HEAVY>())
 void render_basic_kernel(KParams P) {
   extern __shared__ float4 lds_scene[];
   const G::Node* nodes = P.nodes;
@@ -39,10 +46,22 @@ void render_basic_kernel(KParams P) {
 #if defined(__HIP_DEVICE_COMPILE__)
   ws.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)P.walk, 0, (int)P.walk_bytes, 0x00020000);
 #endif
+  /* Q: the scene as shading reads it; HEAVY with perlin_lds: the Perlin tables (turbulence gathers 7 x 8
+   * permutation and gradient entries per noise texture call) staged in LDS behind the walk stream */
+  KParams Q = P;
   if constexpr (WS && LDS) { /* the stream at LDS address 0: its offsets are LDS addresses */
     const float4* g = reinterpret_cast<const float4*>(P.walk);
     const uint32_t staged = HYB ? P.walk_hot : P.walk_bytes;
     for (uint32_t k = threadIdx.x; k < staged / 16u; k += blockDim.x) lds_scene[k] = g[k];
+    if constexpr (HEAVY) {
+      if (P.perlin_lds) {
+        const float4* gp = reinterpret_cast<const float4*>(P.perlin);
+        float4* dst = lds_scene + staged / 16u;
+        const uint32_t n4 = P.n_perlin * (uint32_t)(sizeof(G::Perlin) / 16);
+        for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) dst[k] = gp[k];
+        Q.perlin = reinterpret_cast<const G::Perlin*>(dst);
+      }
+    }
     __syncthreads();
     if (lds_base != 0u) { /* no static LDS in this kernel, so this cannot happen: report, do nothing */
       if (threadIdx.x == 0) atomicOr(&P.stats[12], 2ull);
@@ -185,7 +204,7 @@ void render_basic_kernel(KParams P) {
     if (shading) {
       bool done = true;
       if (traced) {
-        if constexpr (WS) done = shade_walk<COUNT, WMEM, HEAVY>(P, ws, ps, winner, closest, r.o, r.d, r.time, r.tau, sum, cn);
+        if constexpr (WS) done = shade_walk<COUNT, WMEM, HEAVY>(Q, ws, ps, winner, closest, r.o, r.d, r.time, r.tau, sum, cn);
         else done = shade<false, COUNT>(P, ps, winner, closest, r.o, r.d, r.time, r.tau, cn);
         done = done || ps.depth_left == 0;
       }
@@ -230,7 +249,7 @@ void render_basic_kernel(KParams P) {
 template <int CULL, bool COUNT, bool LDS, bool HYB = false, bool HEAVY = false>
 void launch_basic(const KParams& kp, int device, hipStream_t stream, size_t smem) {
   const void* fn = (const void*)render_basic_kernel<CULL, COUNT, LDS, HYB, HEAVY>;
-  const int block = basic_block_threads<LDS>();
+  const int block = basic_block_threads<LDS, sphere_waves<HEAVY>()>();
   /* LDS: the staged scene, then one u32 result slot per thread (layout.h LDS_SCENE_MAX_BYTES leaves
    * room for both, twice per CU) */
   KParams p = kp;
