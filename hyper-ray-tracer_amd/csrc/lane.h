@@ -43,6 +43,7 @@ struct KParams {
   const G::Tex* texs;
   const G::Perlin* perlin;
   const uint8_t* images;
+  const float4* chains; /* layout.h CHAIN_F4 float4 per instance */
   uint32_t main_end;
   float ln_e;
   /* camera (camera.rs:16-31 after resize) */
@@ -380,14 +381,29 @@ HRT_LANE_FI void inst_ray(const G::Inst& in, Vec3& o, Vec3& d) {
 /* The ray in the frame of instance q's children: the world ray through q's enclosing chain, outermost
  * first, exactly as the walk transformed it on the way in (translation.rs:26-30, rotation.rs:104-117).
  * Parent links are followed instead of keeping a per-lane stack (chains are short). */
-HRT_LANE_FI void apply_chain(const KParams& P, uint32_t q, Vec3& o, Vec3& d) {
-  int n = 0;
-  for (uint32_t x = q; x != G::NONE; x = P.insts[x].parent) n++;
-  for (int l = n - 1; l >= 0; l--) {
-    uint32_t x = q;
-    for (int s = 0; s < l; s++) x = P.insts[x].parent;
-    inst_ray(P.insts[x], o, d);
+/* one level of a chain record (layout.h CHAIN_F4): the operations of inst_ray */
+HRT_LANE_FI void chain_level(const float4 v, Vec3& o, Vec3& d) {
+  if (f2u(v.w) == G::I_TRANSLATE) {
+    o = o - v3(v.x, v.y, v.z);
+    return;
   }
+  const int axis = (int)f2u(v.z);
+  int a = (axis + 1) % 3, b = (axis + 2) % 3;
+  float s = v.x, c = v.y;
+  const float oa = comp(o, a), ob = comp(o, b), da = comp(d, a), db = comp(d, b);
+  o = with2(o, a, c * oa + s * ob, b, -s * oa + c * ob);
+  d = with2(d, a, c * da + s * db, b, -s * da + c * db);
+}
+
+/* the first `levels` levels of instance q's chain (all of them: q's children's frame) */
+HRT_LANE_FI void apply_chain_levels(const KParams& P, uint32_t q, uint32_t levels, Vec3& o, Vec3& d) {
+  const float4* c = P.chains + (size_t)q * G::CHAIN_F4;
+  for (uint32_t l = 0; l < levels; l++) chain_level(c[1 + l], o, d);
+}
+
+HRT_LANE_FI void apply_chain(const KParams& P, uint32_t q, Vec3& o, Vec3& d) {
+  if (q == G::NONE) return;
+  apply_chain_levels(P, q, f2u(P.chains[(size_t)q * G::CHAIN_F4].x), o, d);
 }
 
 /* The walk enters instance `in` (K_INST_BEGIN): the ray of its children's frame.  set_dir's derived
@@ -645,19 +661,23 @@ HRT_LANE Rec make_record(const KParams& P, uint32_t winner, float t, Vec3 wo, Ve
       }
     }
     /* back out through the chain, innermost first (translation.rs:32-40, rotation.rs:119-137) */
-    for (uint32_t q = parent; q != G::NONE; q = P.insts[q].parent) {
-      const G::Inst& in = P.insts[q];
-      if ((in.kind & G::I_KIND_MASK) == G::I_TRANSLATE) {
-        rec.p = rec.p + v3(in.d[0], in.d[1], in.d[2]);
-        Vec3 po = wo, pd = wd; /* the ray as q's parent saw it */
-        apply_chain(P, in.parent, po, pd);
-        set_face_normal(rec, pd, rec.n);
-      } else {
-        int a = (int)(in.axis + 1) % 3, b = (int)(in.axis + 2) % 3;
-        float s = in.sin_t, c = in.cos_t;
-        const float pa = comp(rec.p, a), pb = comp(rec.p, b), na = comp(rec.n, a), nb = comp(rec.n, b);
-        rec.p = with2(rec.p, a, c * pa - s * pb, b, s * pa + c * pb);
-        rec.n = with2(rec.n, a, c * na - s * nb, b, s * na + c * nb);
+    if (parent != G::NONE) {
+      const float4* ch = P.chains + (size_t)parent * G::CHAIN_F4;
+      for (int l = (int)f2u(ch[0].x) - 1; l >= 0; l--) {
+        const float4 v = ch[1 + l];
+        if (f2u(v.w) == G::I_TRANSLATE) {
+          rec.p = rec.p + v3(v.x, v.y, v.z);
+          Vec3 po = wo, pd = wd; /* the ray as this level's parent saw it: the chain's first l levels */
+          apply_chain_levels(P, parent, (uint32_t)l, po, pd);
+          set_face_normal(rec, pd, rec.n);
+        } else {
+          const int axis = (int)f2u(v.z);
+          int a = (axis + 1) % 3, b = (axis + 2) % 3;
+          float s = v.x, c = v.y;
+          const float pa = comp(rec.p, a), pb = comp(rec.p, b), na = comp(rec.n, a), nb = comp(rec.n, b);
+          rec.p = with2(rec.p, a, c * pa - s * pb, b, s * pa + c * pb);
+          rec.n = with2(rec.n, a, c * na - s * nb, b, s * na + c * nb);
+        }
       }
     }
     return rec;

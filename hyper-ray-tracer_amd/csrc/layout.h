@@ -71,6 +71,12 @@ struct alignas(16) Inst {
   uint32_t kind;
 };
 
+/* The chain of instance q (what apply_chain applies to reach q's children's frame), outermost first,
+ * CHAIN_F4 float4 per instance: [0].x = the number of levels n (bits), [1..n] = each level's
+ * transform: Translation (dx, dy, dz, I_TRANSLATE), Rotation (sin, cos, axis, I_ROTATE) (bits in z, w).
+ * One record per instance instead of a walk up the parent links: the loads are independent. */
+constexpr uint32_t CHAIN_F4 = MAX_INST_DEPTH + 1;
+
 struct alignas(16) Medium {
   float neg_inv_density;
   uint32_t bstart, bend;

@@ -430,7 +430,8 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
     /* everything leaf programs and shading read, but the Perlin tables and images */
     const size_t ref = s->g_nodes.size() * sizeof(G::Node) + s->g_prims.size() * sizeof(G::Prim) +
                        s->g_insts.size() * sizeof(G::Inst) + s->g_media.size() * sizeof(G::Medium) +
-                       s->g_mats.size() * sizeof(G::Mat) + s->g_texs.size() * sizeof(G::Tex);
+                       s->g_mats.size() * sizeof(G::Mat) + s->g_texs.size() * sizeof(G::Tex) +
+                       s->g_chains.size() * sizeof(float);
     const bool no_lds = (flags & HRT_RENDER_NO_LDS) != 0;
     pl.gwalk_mem = no_lds || walk > LDS_SCENE_MAX ? WM_BUF : (s->w_hot ? WM_HYB : WM_LDS);
     const char* lr = getenv("HRT_GWALK_LREF"); /* A/B knob: "0" keeps the reference stream in global memory */
@@ -522,6 +523,7 @@ KParams scene_params(const hrt_scene* s, const hrt_camera* cam, const hrt_render
   kp.texs = (const G::Tex*)(base + s->off_texs);
   kp.perlin = (const G::Perlin*)(base + s->off_perlin);
   kp.images = (const uint8_t*)(base + s->off_images);
+  kp.chains = (const float4*)(base + s->off_chains);
   kp.main_end = s->main_end;
   kp.ln_e = s->ln_e;
   kp.cam_origin = v3(cam->origin[0], cam->origin[1], cam->origin[2]);

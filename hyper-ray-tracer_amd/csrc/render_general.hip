@@ -75,6 +75,7 @@ void render_gwalk_kernel(KParams P) {
     Q.media = static_cast<const G::Medium*>(stage(P.media, P.n_media, sizeof(G::Medium)));
     Q.mats = static_cast<const G::Mat*>(stage(P.mats, P.n_mats, sizeof(G::Mat)));
     Q.texs = static_cast<const G::Tex*>(stage(P.texs, P.n_texs, sizeof(G::Tex)));
+    Q.chains = static_cast<const float4*>(stage(P.chains, P.n_insts, G::CHAIN_F4 * 16u));
     if (P.perlin_lds) Q.perlin = static_cast<const G::Perlin*>(stage(P.perlin, P.n_perlin, sizeof(G::Perlin)));
     nodes = Q.nodes;
     prims = Q.prims;

@@ -688,6 +688,24 @@ void flatten(hrt_scene* s) {
     s->g_media[f.pending[i].medium].bend = (uint32_t)s->g_nodes.size();
   }
   for (const G::Medium& m : s->g_media) s->feature_mask |= tex_features(s, s->g_mats[m.mat].tex);
+  /* every instance's chain, outermost first (layout.h CHAIN_F4) */
+  s->g_chains.assign(s->g_insts.size() * G::CHAIN_F4 * 4, 0.0f);
+  for (uint32_t q = 0; q < (uint32_t)s->g_insts.size(); q++) {
+    std::vector<uint32_t> ids;
+    for (uint32_t x = q; x != G::NONE; x = s->g_insts[x].parent) ids.push_back(x);
+    need(ids.size() <= G::MAX_INST_DEPTH, HRT_ERR_UNSUPPORTED, "instances nested deeper than 8");
+    float* c = &s->g_chains[(size_t)q * G::CHAIN_F4 * 4];
+    c[0] = u2f((uint32_t)ids.size());
+    for (size_t l = 0; l < ids.size(); l++) {
+      const G::Inst& in = s->g_insts[ids[ids.size() - 1 - l]];
+      float* v = c + 4 * (1 + l);
+      if ((in.kind & G::I_KIND_MASK) == G::I_TRANSLATE) {
+        v[0] = in.d[0]; v[1] = in.d[1]; v[2] = in.d[2]; v[3] = u2f(G::I_TRANSLATE);
+      } else {
+        v[0] = in.sin_t; v[1] = in.cos_t; v[2] = u2f(in.axis); v[3] = u2f(G::I_ROTATE);
+      }
+    }
+  }
   /* Default culling: the reference's per-axis test AND the provably safe inflated slab test
    * (layout.h CULL_EXACT; boxes that may not hold their geometry are flagged NODE_REF_ONLY). */
   bool sphere_only = (s->feature_mask & (G::F_RECT | G::F_INSTANCE | G::F_MEDIUM)) == 0;
@@ -1270,6 +1288,7 @@ std::vector<uint8_t> build_blob(hrt_scene* s) {
   s->off_texs = section(s->g_texs.size() * sizeof(G::Tex));
   s->off_perlin = section(s->perlin.size() * sizeof(G::Perlin));
   s->off_images = section(s->images.size());
+  s->off_chains = section(s->g_chains.size() * sizeof(float));
   s->off_fnodes = section(s->f_nodes.size() * sizeof(G::Node));
   s->off_fprims = section(s->f_prims.size() * sizeof(G::Prim));
   s->off_walk = section(s->w_stream.size() * sizeof(float));
@@ -1286,6 +1305,7 @@ std::vector<uint8_t> build_blob(hrt_scene* s) {
   put(s->off_texs, s->g_texs.data(), s->g_texs.size() * sizeof(G::Tex));
   put(s->off_perlin, s->perlin.data(), s->perlin.size() * sizeof(G::Perlin));
   put(s->off_images, s->images.data(), s->images.size());
+  put(s->off_chains, s->g_chains.data(), s->g_chains.size() * sizeof(float));
   put(s->off_fnodes, s->f_nodes.data(), s->f_nodes.size() * sizeof(G::Node));
   put(s->off_fprims, s->f_prims.data(), s->f_prims.size() * sizeof(G::Prim));
   put(s->off_walk, s->w_stream.data(), s->w_stream.size() * sizeof(float));
@@ -1703,6 +1723,7 @@ hrt_status hrt_debug_scene_blob(hrt_scene* s, void* out, uint64_t cap, uint64_t*
       info->bvh_tied_sorts = s->bvh_tied_sorts;
       info->walk_hot = s->w_hot;
       info->walk_general = s->w_general ? 1u : 0u;
+      info->off_chains = s->off_chains;
     }
   });
 }

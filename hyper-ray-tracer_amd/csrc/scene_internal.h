@@ -107,6 +107,7 @@ struct hrt_scene {
   std::vector<hrt::gpu::Medium> g_media;
   std::vector<hrt::gpu::Mat> g_mats;
   std::vector<hrt::gpu::Tex> g_texs;
+  std::vector<float> g_chains; /* layout.h CHAIN_F4 float4 per instance */
   uint32_t main_end = 0;
   /* SAH fast path (sphere-only scenes, slab culling): 8 pre-order streams of equal length, one per
    * ray-direction octant (near child first), over a reordered copy of the primitives. */
@@ -140,7 +141,7 @@ struct hrt_scene {
   void* d_blob = nullptr;
   size_t blob_bytes = 0;
   size_t off_nodes = 0, off_prims = 0, off_insts = 0, off_media = 0, off_mats = 0, off_texs = 0,
-         off_perlin = 0, off_images = 0;
+         off_perlin = 0, off_images = 0, off_chains = 0;
   /* Render scratch slots (allocated at commit, reused round-robin): device [counter | stats |
    * tiles], a pinned host staging copy of the tile list, and the event that marks the end of the
    * slot's last use.  A call waits for its slot's previous use, so calls on any streams are safe. */

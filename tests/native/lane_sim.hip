@@ -143,6 +143,7 @@ int lane_sim_render(const void* blob, const hrt_blob_info* bi, const hrt_camera*
   P.texs = (const G::Tex*)(base + bi->off_texs);
   P.perlin = (const G::Perlin*)(base + bi->off_perlin);
   P.images = base + bi->off_images;
+  P.chains = (const float4*)(base + bi->off_chains);
   P.main_end = bi->main_end;
   P.ln_e = bi->ln_e;
   P.motion_uniform = bi->motion_uniform;
