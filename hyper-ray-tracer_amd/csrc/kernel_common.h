@@ -76,7 +76,7 @@ __device__ __forceinline__ void stage_scene(const KParams& P, float4* lds, const
 
 /* A lane's current work item: one pixel and a chunk [sample, sample_end) of its samples.  slot: where
  * the chunk's result goes, P.out[slot] (one chunk) or P.partial[slot] = [n_out][chunk] (the host checks
- * n_chunks x n_out < 2^32); the chunk is first iff sample_end <= P.chunk. */
+ * n_chunks x n_out < 2^32); the chunk is first iff sample_end <= P.chunk (lane.h chunk_plan). */
 struct Item {
   uint32_t pxy; /* px | py << 16 */
   uint32_t slot, sample, sample_end;
@@ -89,10 +89,10 @@ struct WaveBlock {
 constexpr uint32_t CLAIM_BLOCK = 64; /* items per atomicAdd on the work counter */
 
 /* Idle lanes of the wave take work items from the wave's block (ballot + popcount); when it runs short
- * the wave claims the next CLAIM_BLOCK items with ONE atomicAdd.  Items are ordered [tile][8x8 block]
- * [chunk][64 pixels], so a block is one chunk of 64 neighbouring pixels.  A wave hands out its whole
- * block before it claims another, and its lanes retire only on an item past the end, so no item is
- * left behind. */
+ * the wave claims the next CLAIM_BLOCK items with ONE atomicAdd.  Items are ordered [chunk][tile]
+ * [8x8 block][64 pixels] (chunk-major: the short tail chunks of lane.h chunk_plan come last), so a block
+ * is one chunk of 64 neighbouring pixels.  A wave hands out its whole block before it claims another,
+ * and its lanes retire only on an item past the end, so no item is left behind. */
 __device__ __forceinline__ void claim_work(const KParams& P, uint32_t lane, bool& has_item, bool& exhausted,
                                            Item& it, WaveBlock& wb) {
   const bool want = !has_item && !exhausted;
@@ -121,29 +121,29 @@ __device__ __forceinline__ void claim_work(const KParams& P, uint32_t lane, bool
     exhausted = true;
     return;
   }
-  /* tile (tiles padded to one stride: a division; else a binary search on pad_start), then [8x8 block]
-   * [chunk][64 pixels] inside it */
+  /* the chunk, then the tile (tiles padded to one stride: a division; else a binary search on
+   * pad_start, in padded pixels), then [8x8 block][64 pixels] inside it */
+  const uint32_t c = w / P.pad_px;
+  const uint32_t px = w - c * P.pad_px;
   uint32_t lo = 0;
   if (P.tile_stride) {
-    lo = w / P.tile_stride;
+    lo = px / P.tile_stride;
   } else {
     uint32_t hi = P.n_tiles - 1;
     while (lo < hi) {
       uint32_t mid = (lo + hi + 1) >> 1;
-      if (P.tiles[mid].pad_start <= w) lo = mid; else hi = mid - 1;
+      if (P.tiles[mid].pad_start <= px) lo = mid; else hi = mid - 1;
     }
   }
   const G::TileDev T = P.tiles[lo];
-  const uint32_t q = w - T.pad_start;
-  const uint32_t blk = q / (64u * P.n_chunks), rem = q - blk * 64u * P.n_chunks;
-  const uint32_t c = rem >> 6, in = rem & 63u;
+  const uint32_t q = px - T.pad_start;
+  const uint32_t blk = q >> 6, in = q & 63u;
   const uint32_t lx = (blk % T.bw) * 8u + (in & 7u), ly = (blk / T.bw) * 8u + (in >> 3);
   if (lx < T.w && ly < T.h) {
     has_item = true;
     it.pxy = (T.x + lx) | ((T.y + ly) << 16);
     it.slot = (T.out_off + ly * T.w + lx) * P.n_chunks + c;
-    it.sample = c * P.chunk;
-    it.sample_end = min(P.spp, it.sample + P.chunk);
+    chunk_range(P, c, it.sample, it.sample_end);
   }
 }
 

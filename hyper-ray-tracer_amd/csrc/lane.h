@@ -64,8 +64,10 @@ struct KParams {
   uint32_t* counter;
   uint32_t claim_fine; /* work items from here on are claimed one per lane (kernel_common.h claim_work) */
   unsigned long long* stats; /* segments, samples, pixels, then (COUNT builds) nodes, prims, tex */
-  /* sample chunks: a work item is (pixel, chunk of `chunk` consecutive samples) */
+  /* sample chunks: a work item is (pixel, chunk of consecutive samples); lane.h chunk_range */
   uint32_t chunk, n_chunks, n_out;
+  uint32_t chunk_head, chunk_first; /* head chunks (the first holds chunk_first samples, the rest `chunk`) */
+  uint32_t pad_px;                  /* padded pixels of the call's tiles: items are [chunk][tile][8x8 block][64] */
   uint32_t n_prims;
   uint32_t n_nodes;    /* node-stream entries to stage in LDS */
   uint32_t stream_len; /* FAST: length of one octant stream */
@@ -107,6 +109,41 @@ inline uint32_t sample_chunk(uint32_t spp, uint32_t cls, uint32_t cmin = 0, uint
   if (cdiv == 0) cdiv = cls == CHUNK_SPHERE ? 32u : 8u;
   const uint32_t even = (spp + cdiv - 1) / cdiv;
   return spp <= cmin ? spp : (even > cmin ? even : cmin);
+}
+
+/* The chunks of a pixel's spp samples (r03): HEAD chunks of c samples (the first holds the remainder r),
+ * then a TAIL of halving chunks c/2, c/2, c/4, c/4, ..., 1, 1.  Items run chunk-major ([chunk][tile]
+ * [8x8 block][64 pixels]), so a launch ends on the tail's short items instead of full chunks: the last
+ * items run with the device mostly idle, and their length was the loss of small launches (one GPU's
+ * 1/8 share of C2 ran at 84% of the whole frame's rate with uniform 16-sample chunks).  The schedule
+ * depends on spp and c alone, so every tile split sums a pixel's samples in the same chunks, added in
+ * chunk order.  No tail when it would leave less than one head chunk, or with tail = false. */
+inline void chunk_plan(uint32_t spp, uint32_t c, bool tail, uint32_t& n_head, uint32_t& first, uint32_t& n_tail) {
+  uint32_t T = 0, L = 0;
+  if (tail && spp > c)
+    for (uint32_t m = 1; (c >> m) >= 1u; m++) {
+      T += 2u * (c >> m);
+      L++;
+    }
+  if (T > 0 && (spp - c < T)) T = L = 0; /* spp - T < c */
+  const uint32_t H = spp - T;
+  n_head = (H + c - 1) / c;
+  first = H - (n_head - 1) * c;
+  n_tail = 2u * L;
+}
+
+/* samples [s0, s1) of chunk k */
+HRT_LANE_FI void chunk_range(const KParams& P, uint32_t k, uint32_t& s0, uint32_t& s1) {
+  if (k < P.chunk_head) {
+    s0 = k == 0 ? 0u : P.chunk_first + (k - 1u) * P.chunk;
+    s1 = P.chunk_first + k * P.chunk;
+    return;
+  }
+  const uint32_t j = k - P.chunk_head;
+  uint32_t s = P.chunk_first + (P.chunk_head - 1u) * P.chunk;
+  for (uint32_t i = 0; i < j; i++) s += P.chunk >> (1u + (i >> 1));
+  s0 = s;
+  s1 = s + (P.chunk >> (1u + (j >> 1)));
 }
 
 /* per-lane work counters of the instrumented (COUNT) instantiation */

@@ -731,7 +731,10 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     const char* cd = getenv("HRT_CHUNK_DIV"); /* A/B knob: at most this many chunks (default 32 / 8) */
     const uint32_t cdiv = cd && atoi(cd) > 0 ? (uint32_t)atoi(cd) : 0u;
     const uint32_t chunk = sample_chunk(spp, chunk_class(s->feature_mask, s->main_end), cmin, cdiv);
-    const uint32_t n_chunks = (spp + chunk - 1) / chunk;
+    const char* ct = getenv("HRT_CHUNK_TAIL"); /* A/B knob: "0" = uniform chunks (no halving tail) */
+    uint32_t n_head = 0, first = 0, n_tail = 0;
+    chunk_plan(spp, chunk, !(ct && strcmp(ct, "0") == 0), n_head, first, n_tail);
+    const uint32_t n_chunks = n_head + n_tail;
     std::vector<G::TileDev> td(n_tiles);
     uint64_t pad = 0, outp = 0;
     for (uint32_t i = 0; i < n_tiles; i++) {
@@ -740,7 +743,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
         throw HipError{HRT_ERR_INVALID_ARG, "tile outside the image"};
       uint32_t bw = (t.w + 7) / 8, bh = (t.h + 7) / 8;
       td[i] = G::TileDev{t.x, t.y, t.w, t.h, bw, (uint32_t)pad, (uint32_t)outp, 0};
-      pad += (uint64_t)bw * bh * 64 * n_chunks;
+      pad += (uint64_t)bw * bh * 64; /* padded pixels (items: pad x n_chunks, chunk-major) */
       outp += (uint64_t)t.w * t.h;
     }
     /* Many tiles (a rank's share of the 16-px grid: 4080 tiles at 2 GPUs): a claim's binary search over
@@ -750,17 +753,17 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     uint32_t stride = 0;
     if (n_tiles > 1) {
       uint64_t mx = 0;
-      for (uint32_t i = 0; i < n_tiles; i++) mx = std::max<uint64_t>(mx, (uint64_t)((td[i].w + 7) / 8) * ((td[i].h + 7) / 8) * 64 * n_chunks);
+      for (uint32_t i = 0; i < n_tiles; i++) mx = std::max<uint64_t>(mx, (uint64_t)((td[i].w + 7) / 8) * ((td[i].h + 7) / 8) * 64);
       const char* ts = getenv("HRT_TILE_STRIDE"); /* A/B knob: "0" keeps the binary search */
-      if (mx * n_tiles <= pad + pad / 8 && mx * n_tiles < 0xF0000000ull && !(ts && strcmp(ts, "0") == 0)) {
+      if (mx * n_tiles <= pad + pad / 8 && mx * n_tiles * n_chunks < 0xF0000000ull && !(ts && strcmp(ts, "0") == 0)) {
         stride = (uint32_t)mx;
         for (uint32_t i = 0; i < n_tiles; i++) td[i].pad_start = i * stride;
         pad = mx * n_tiles;
       }
     }
-    /* work items and Item.slot (pixel x n_chunks + chunk < pad) are 32-bit */
+    /* work items and Item.slot (pixel x n_chunks + chunk < pad x n_chunks) are 32-bit */
     /* headroom: waves claim blocks of CLAIM_BLOCK items past the end before they retire */
-    if (pad >= 0xF0000000ull) throw HipError{HRT_ERR_UNSUPPORTED, "more than 3.75G pixel x sample-chunk items in one call"};
+    if (pad * n_chunks >= 0xF0000000ull) throw HipError{HRT_ERR_UNSUPPORTED, "more than 3.75G pixel x sample-chunk items in one call"};
     hipStream_t stream = (hipStream_t)stream_;
     DeviceGuard dg(s->device);
     /* scratch slot: device [counter u32 | pad | stats 8 x u64 | pad to HDR | tiles], pinned host [stats | tiles] */
@@ -814,7 +817,8 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     KParams kp = scene_params(s, cam, p, pl);
     kp.tiles = (const G::TileDev*)((uint8_t*)scratch + SLOT_HDR);
     kp.n_tiles = n_tiles;
-    kp.total_work = (uint32_t)pad;
+    kp.total_work = (uint32_t)(pad * n_chunks);
+    kp.pad_px = (uint32_t)pad;
     kp.tile_stride = stride;
     /* the sphere kernel claims blocks of items to the end: its passes are short, and per-lane claims
      * made them wait on the contended counter (r02y: +12% on C2; per-lane claims for the last 0.26 /
@@ -824,13 +828,16 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
      * HRT_CLAIM_FINE (A/B knob): claim the last that many items per lane, in every kernel */
     const bool sphere_kernel = (!pl.full && !pl.fast && !pl.general) || pl.gwalk; /* block claims */
     const char* cf = getenv("HRT_CLAIM_FINE");
-    const uint64_t fine = cf ? strtoull(cf, nullptr, 10) : (sphere_kernel ? 0u : pad);
-    kp.claim_fine = (uint32_t)(pad > fine ? pad - fine : 0);
+    const uint64_t work = pad * n_chunks;
+    const uint64_t fine = cf ? strtoull(cf, nullptr, 10) : (sphere_kernel ? 0u : work);
+    kp.claim_fine = (uint32_t)(work > fine ? work - fine : 0);
     kp.out = (float4*)d_rgba;
     kp.counter = (uint32_t*)scratch;
     kp.stats = (unsigned long long*)((uint8_t*)scratch + 8);
     kp.chunk = chunk;
     kp.n_chunks = n_chunks;
+    kp.chunk_head = n_head;
+    kp.chunk_first = first;
     kp.n_out = (uint32_t)outp;
     kp.partial = (float4*)sl.d_partial;
     if (p->flags & HRT_RENDER_COUNT_WORK) launch_any<true>(s, pl, kp, stream);

@@ -11,6 +11,7 @@
  * tests/test_lane_sim.py checks it against the CPU oracle (oracle/) without a GPU.  It is built by the
  * tests (host-only compile) and is not part of libhrt.
  */
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -27,15 +28,15 @@ template <int CULL, int KIND>
 void render_pixel(const KParams& P, uint32_t px, uint32_t py, float* rgba, uint64_t* cnt) {
   constexpr bool FULL = KIND == 1;
   const uint32_t spp = P.spp;
-  const uint32_t chunk = P.chunk; /* render.hip: lane.h sample_chunk, set by the caller */
-  const uint32_t n_chunks = (spp + chunk - 1) / chunk;
+  const uint32_t n_chunks = P.n_chunks; /* render.hip: lane.h sample_chunk + chunk_plan, set by the caller */
   const float inf = u2f(0x7f800000u);
   Counts cn{0u, 0u, 0u, 0u, 0u, 0u};
   Vec3 total = v3(0.0f, 0.0f, 0.0f);
   for (uint32_t c = 0; c < n_chunks; c++) {
     Vec3 sum = v3(0.0f, 0.0f, 0.0f);
-    const uint32_t s_end = std::min(spp, (c + 1) * chunk);
-    for (uint32_t sample = c * chunk; sample < s_end; sample++) {
+    uint32_t s_begin, s_end;
+    chunk_range(P, c, s_begin, s_end);
+    for (uint32_t sample = s_begin; sample < s_end; sample++) {
       PathState ps;
       init_path_state(ps);
       start_sample(P, ps, px, py, sample);
@@ -126,6 +127,22 @@ void render_pixel(const KParams& P, uint32_t px, uint32_t py, float* rgba, uint6
 
 extern "C" {
 
+/* the sample chunks of a pixel (lane.h chunk_plan / chunk_range): ranges[2k], ranges[2k+1] = [s0, s1) of
+ * chunk k; returns the number of chunks (the caller's cap permitting) */
+int lane_sim_chunks(uint32_t spp, uint32_t cls, int tail, uint32_t* ranges, uint32_t cap) {
+  KParams P;
+  memset(&P, 0, sizeof(P));
+  P.spp = spp;
+  P.chunk = sample_chunk(spp, cls);
+  uint32_t nh = 0, first = 0, nt = 0;
+  chunk_plan(spp, P.chunk, tail != 0, nh, first, nt);
+  P.chunk_head = nh;
+  P.chunk_first = first;
+  P.n_chunks = nh + nt;
+  for (uint32_t k = 0; k < P.n_chunks && k < cap; k++) chunk_range(P, k, ranges[2 * k], ranges[2 * k + 1]);
+  return (int)P.n_chunks;
+}
+
 /* kernel: 0 = render_basic_kernel's lane, 1 = render_full_kernel's, 2 = render_kernel's (segment
  * at a time), 3 = render_gwalk_kernel's (general walk stream; CULL_EXACT); cull: layout.h CULL_*.
  * cnt[0..4] += segments, samples, node visits, primitive tests, texture evaluations. */
@@ -167,6 +184,14 @@ int lane_sim_render(const void* blob, const hrt_blob_info* bi, const hrt_camera*
   set_pixel_rcp(P);
   P.spp = p->samples;
   P.chunk = sample_chunk(P.spp, chunk_class(bi->feature_mask, bi->main_end));
+  {
+    const char* ct = getenv("HRT_CHUNK_TAIL");
+    uint32_t nh = 0, first = 0, nt = 0;
+    chunk_plan(P.spp, P.chunk, !(ct && strcmp(ct, "0") == 0), nh, first, nt);
+    P.chunk_head = nh;
+    P.chunk_first = first;
+    P.n_chunks = nh + nt;
+  }
   P.max_depth = p->max_depth;
   P.sample_offset = p->sample_offset;
   P.t_min = p->t_min;

@@ -42,6 +42,8 @@ def sim(tmp_path_factory):
                     os.path.join(HERE, "native", "lane_sim.hip"), "-o", so], check=True)
     L = ctypes.CDLL(so)
     L.lane_sim_render.restype = ctypes.c_int
+    L.lane_sim_chunks.restype = ctypes.c_int
+    L.lane_sim_chunks.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32]
     return L
 
 
@@ -233,3 +235,34 @@ def test_group_box_is_tested_once_per_group(sim, earth):
     ref, cnt = oracle_render("cornell", 2048, 2048, 1250, 50, 1, earth, region=region)
     assert st["segments"] == cnt["segments"] == 12578
     assert np.abs(img - ref).max() <= TOL
+
+
+def _chunks(L, spp, cls, tail=1):
+    buf = (ctypes.c_uint32 * 4096)()
+    n = L.lane_sim_chunks(spp, cls, tail, buf, 2048)
+    return [(buf[2 * k], buf[2 * k + 1]) for k in range(n)]
+
+
+@pytest.mark.parametrize("spp", [1, 7, 16, 17, 40, 64, 70, 100, 500, 1000, 1250, 2000, 10000])
+@pytest.mark.parametrize("cls", [0, 1, 2])
+def test_sample_chunks_partition_the_samples(sim, spp, cls):
+    """lane.h chunk_plan: head chunks of c samples (the first holds the remainder), then a halving tail
+    c/2, c/2, ..., 1, 1; the chunks partition [0, spp) in order, and the first chunk is the only one that
+    ends at or before c (the kernels count a pixel once, at its first chunk)."""
+    ch = _chunks(sim, spp, cls)
+    assert ch[0][0] == 0 and ch[-1][1] == spp
+    assert all(a[1] == b[0] for a, b in zip(ch, ch[1:]))
+    assert all(s1 > s0 for s0, s1 in ch)
+    uni = _chunks(sim, spp, cls, tail=0)
+    c = max(s1 - s0 for s0, s1 in uni)
+    assert [s1 <= c for _, s1 in ch].count(True) == 1
+    sizes = [s1 - s0 for s0, s1 in ch]
+    if len(ch) > len(uni):  # a tail: non-increasing sizes after the head, ending in single samples
+        tail = sizes[len(ch) - 2 * (c.bit_length() - 1):]
+        assert tail == sorted(tail, reverse=True) and tail[-2:] == [1, 1]
+
+
+def test_sample_chunks_of_the_headline_frame(sim):
+    """C2 (500 spp, sphere class): 30 head chunks (6, then 29 of 16) and the tail 8, 8, 4, 4, 2, 2, 1, 1."""
+    sizes = [b - a for a, b in _chunks(sim, 500, 0)]
+    assert sizes == [6] + [16] * 29 + [8, 8, 4, 4, 2, 2, 1, 1]
