@@ -89,9 +89,9 @@ struct WaveBlock {
 constexpr uint32_t CLAIM_BLOCK = 64; /* items per atomicAdd on the work counter */
 
 /* Idle lanes of the wave take work items from the wave's block (ballot + popcount); when it runs short
- * the wave claims the next CLAIM_BLOCK items with ONE atomicAdd.  Items are ordered [chunk][tile]
- * [8x8 block][64 pixels] (chunk-major: the short tail chunks of lane.h chunk_plan come last), so a block
- * is one chunk of 64 neighbouring pixels.  A wave hands out its whole block before it claims another,
+ * the wave claims the next CLAIM_BLOCK items with ONE atomicAdd.  Items are the head chunks' (lane.h
+ * chunk_plan) ordered [tile][8x8 block][chunk][64 pixels], then the short tail chunks' chunk-major, so
+ * the launch ends on short items; a block is one chunk of 64 neighbouring pixels.  A wave hands out its whole block before it claims another,
  * and its lanes retire only on an item past the end, so no item is left behind. */
 __device__ __forceinline__ void claim_work(const KParams& P, uint32_t lane, bool& has_item, bool& exhausted,
                                            Item& it, WaveBlock& wb) {
@@ -121,10 +121,20 @@ __device__ __forceinline__ void claim_work(const KParams& P, uint32_t lane, bool
     exhausted = true;
     return;
   }
-  /* the chunk, then the tile (tiles padded to one stride: a division; else a binary search on
-   * pad_start, in padded pixels), then [8x8 block][64 pixels] inside it */
-  const uint32_t c = w / P.pad_px;
-  const uint32_t px = w - c * P.pad_px;
+  /* head items [tile][8x8 block][head chunk][64 pixels] (a wave works through one block's chunks in a
+   * row: its pixels' texels and partial sums stay in cache), then the tail items chunk-major
+   * [tail chunk][tile][8x8 block][64 pixels]; px = the padded pixel, then its tile (tiles padded to one
+   * stride: a division; else a binary search on pad_start) */
+  uint32_t c, px;
+  if (w < P.head_items) {
+    const uint32_t g = w / (64u * P.chunk_head), rem = w - g * 64u * P.chunk_head;
+    c = rem >> 6;
+    px = g * 64u + (rem & 63u);
+  } else {
+    const uint32_t t = w - P.head_items, k = t / P.pad_px;
+    c = P.chunk_head + k;
+    px = t - k * P.pad_px;
+  }
   uint32_t lo = 0;
   if (P.tile_stride) {
     lo = px / P.tile_stride;

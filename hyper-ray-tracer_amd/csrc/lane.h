@@ -67,7 +67,8 @@ struct KParams {
   /* sample chunks: a work item is (pixel, chunk of consecutive samples); lane.h chunk_range */
   uint32_t chunk, n_chunks, n_out;
   uint32_t chunk_head, chunk_first; /* head chunks (the first holds chunk_first samples, the rest `chunk`) */
-  uint32_t pad_px;                  /* padded pixels of the call's tiles: items are [chunk][tile][8x8 block][64] */
+  uint32_t pad_px;                  /* padded pixels of the call's tiles */
+  uint32_t head_items;              /* pad_px x chunk_head: the head chunks' items come first (claim_work) */
   uint32_t n_prims;
   uint32_t n_nodes;    /* node-stream entries to stage in LDS */
   uint32_t stream_len; /* FAST: length of one octant stream */
@@ -112,16 +113,16 @@ inline uint32_t sample_chunk(uint32_t spp, uint32_t cls, uint32_t cmin = 0, uint
 }
 
 /* The chunks of a pixel's spp samples (r03): HEAD chunks of c samples (the first holds the remainder r),
- * then a TAIL of halving chunks c/2, c/2, c/4, c/4, ..., 1, 1.  Items run chunk-major ([chunk][tile]
- * [8x8 block][64 pixels]), so a launch ends on the tail's short items instead of full chunks: the last
+ * then a TAIL of halving chunks c/2, c/2, c/4, c/4, ..., 1, 1.  The tail's items run last, chunk-major
+ * (kernel_common.h claim_work), so a launch ends on short items instead of full chunks: the last
  * items run with the device mostly idle, and their length was the loss of small launches (one GPU's
  * 1/8 share of C2 ran at 84% of the whole frame's rate with uniform 16-sample chunks).  The schedule
  * depends on spp and c alone, so every tile split sums a pixel's samples in the same chunks, added in
  * chunk order.  No tail when it would leave less than one head chunk, or with tail = false. */
-inline void chunk_plan(uint32_t spp, uint32_t c, bool tail, uint32_t& n_head, uint32_t& first, uint32_t& n_tail) {
+inline void chunk_plan(uint32_t spp, uint32_t c, uint32_t levels, uint32_t& n_head, uint32_t& first, uint32_t& n_tail) {
   uint32_t T = 0, L = 0;
-  if (tail && spp > c)
-    for (uint32_t m = 1; (c >> m) >= 1u; m++) {
+  if (levels && spp > c)
+    for (uint32_t m = 1; (c >> m) >= 1u && m <= levels; m++) {
       T += 2u * (c >> m);
       L++;
     }

@@ -731,9 +731,9 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     const char* cd = getenv("HRT_CHUNK_DIV"); /* A/B knob: at most this many chunks (default 32 / 8) */
     const uint32_t cdiv = cd && atoi(cd) > 0 ? (uint32_t)atoi(cd) : 0u;
     const uint32_t chunk = sample_chunk(spp, chunk_class(s->feature_mask, s->main_end), cmin, cdiv);
-    const char* ct = getenv("HRT_CHUNK_TAIL"); /* A/B knob: "0" = uniform chunks (no halving tail) */
+    const char* ct = getenv("HRT_CHUNK_TAIL"); /* A/B knob: halving levels of the tail ("0" = uniform chunks) */
     uint32_t n_head = 0, first = 0, n_tail = 0;
-    chunk_plan(spp, chunk, !(ct && strcmp(ct, "0") == 0), n_head, first, n_tail);
+    chunk_plan(spp, chunk, ct ? (uint32_t)atoi(ct) : 32u, n_head, first, n_tail);
     const uint32_t n_chunks = n_head + n_tail;
     std::vector<G::TileDev> td(n_tiles);
     uint64_t pad = 0, outp = 0;
@@ -819,6 +819,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     kp.n_tiles = n_tiles;
     kp.total_work = (uint32_t)(pad * n_chunks);
     kp.pad_px = (uint32_t)pad;
+    kp.head_items = (uint32_t)(pad * n_head);
     kp.tile_stride = stride;
     /* the sphere kernel claims blocks of items to the end: its passes are short, and per-lane claims
      * made them wait on the contended counter (r02y: +12% on C2; per-lane claims for the last 0.26 /

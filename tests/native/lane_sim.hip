@@ -135,7 +135,7 @@ int lane_sim_chunks(uint32_t spp, uint32_t cls, int tail, uint32_t* ranges, uint
   P.spp = spp;
   P.chunk = sample_chunk(spp, cls);
   uint32_t nh = 0, first = 0, nt = 0;
-  chunk_plan(spp, P.chunk, tail != 0, nh, first, nt);
+  chunk_plan(spp, P.chunk, tail, nh, first, nt);
   P.chunk_head = nh;
   P.chunk_first = first;
   P.n_chunks = nh + nt;
@@ -187,7 +187,7 @@ int lane_sim_render(const void* blob, const hrt_blob_info* bi, const hrt_camera*
   {
     const char* ct = getenv("HRT_CHUNK_TAIL");
     uint32_t nh = 0, first = 0, nt = 0;
-    chunk_plan(P.spp, P.chunk, !(ct && strcmp(ct, "0") == 0), nh, first, nt);
+    chunk_plan(P.spp, P.chunk, ct ? (uint32_t)atoi(ct) : 32u, nh, first, nt);
     P.chunk_head = nh;
     P.chunk_first = first;
     P.n_chunks = nh + nt;

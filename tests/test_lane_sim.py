@@ -237,7 +237,7 @@ def test_group_box_is_tested_once_per_group(sim, earth):
     assert np.abs(img - ref).max() <= TOL
 
 
-def _chunks(L, spp, cls, tail=1):
+def _chunks(L, spp, cls, tail=32):
     buf = (ctypes.c_uint32 * 4096)()
     n = L.lane_sim_chunks(spp, cls, tail, buf, 2048)
     return [(buf[2 * k], buf[2 * k + 1]) for k in range(n)]
