@@ -157,6 +157,8 @@ struct Counts {
 
 struct TRay {
   Vec3 o, d, inv;
+  Vec3 noinv; /* -(o * inv) per axis for the walk's inflated test (box_ce); NaN in all three when an inv
+                 or a product is not a finite normal number (every inflated test then passes) */
   float time;
   float dd;  /* dot(d, d): sphere.rs:42 `a`, constant for the ray */
   float rdd; /* RN(1 / dd) for div_rn, or NaN when dd is outside div_rn's fast domain */
@@ -201,6 +203,14 @@ HRT_LANE_FI void set_dir(TRay& r, Vec3 o, Vec3 d) {
   r.d = d;
   /* aabb.rs:22 computes 1/d per call; the value is the same every time */
   r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  r.noinv = v3(-(o.x * r.inv.x), -(o.y * r.inv.y), -(o.z * r.inv.z));
+  /* box_ce's D is exact only for a normal |inv| (a zero or denormal inv drops its axis from D) and a
+   * finite product: otherwise the walk keeps no inflated culling for this ray (the leaves' reference
+   * test still decides) */
+  auto normal = [](float x) { return (int)(fabsf(x) >= 0x1p-126f) & (int)(fabsf(x) <= 3.40282347e+38f); }; /* 0 on NaN */
+  auto finite = [](float x) { return (int)(fabsf(x) <= 3.40282347e+38f); };
+  if (!(normal(r.inv.x) & normal(r.inv.y) & normal(r.inv.z) & finite(r.noinv.x) & finite(r.noinv.y) & finite(r.noinv.z)))
+    r.noinv = v3(u2f(0x7fc00000u), u2f(0x7fc00000u), u2f(0x7fc00000u));
   r.dd = dot(d, d);
   r.rdd = div_rn_y(r.dd);
 }
@@ -1159,24 +1169,50 @@ HRT_LANE_FI void basic_step(const KParams& P, const G::Node* __restrict__ nodes,
  * max_k |C_k - o_k| + E_k >= the L-inf distance of its farthest point from the origin), misses the ray
  * on [tmin, tmax].  Per axis the slab is m_k -+ t_k |inv_k| with m_k = (C_k - o_k) inv_k and
  * t_k = E_k + EXACT_MARGIN D', so the near/far swap of aabb.rs:28-29 disappears; each bound is one fma
- * (t_k by fmamk, the bounds by fma with |inv_k| as a source modifier: 21 VALU per box).  Rounding errors
- * of the whole computation stay below ~6 2^-24 D' |inv_k|, far inside the slack of EXACT_MARGIN
- * (layout.h: 4e-3 covers the 2.4e-3 needed 1.65 times).  A NaN bound (inv_k = +-inf: C_k = o_k or
- * E_k = 0) is ignored by max3/min3: no constraint.  An infinite box (E = +inf) always passes. */
+ * (t_k by fmamk, the bounds by fma with |inv_k| as a source modifier).
+ * HRT_BOX_FMA (default): m_k = fma(C_k, inv_k, -(o_k inv_k)) with the product kept per ray (TRay.noinv)
+ * and |C_k - o_k| = |m_k| |d_k| folded into e_k = fma(|m_k|, |d_k|, E_k): two instructions per axis
+ * instead of three (sub, mul, add).  Its extra error is the rounding of o_k inv_k, 2^-24 |o_k| in
+ * position units; the stream's boxes keep max_k E_k >= 2^-12 max_k |C_k| (layout.h CE_FLOOR), so
+ * |o_k| <= |C_k| + D' <= 4097 D' and that error stays below 2.5e-4 D'.  Rounding errors of the whole
+ * computation stay below ~2.6e-4 D' |inv_k|, inside the slack of EXACT_MARGIN (layout.h: 4e-3 covers the
+ * 2.4e-3 needed with 1.6e-3 to spare).  A NaN bound (the old form: inv_k = +-inf with C_k = o_k or
+ * E_k = 0) is ignored by max3/min3: no constraint; a ray whose noinv is NaN (set_dir) passes every box.
+ * An infinite box (E = +inf) always passes.  The hybrid LDS / global walk (WM_HYB, latency-bound) keeps
+ * the sub/mul/add form: the three more live registers cost it 4.5% (C4 1/8 share), while the LDS walks
+ * gain 1.5% (C2) from the two fewer instructions per axis. */
+#ifndef HRT_BOX_FMA
+#define HRT_BOX_FMA 1
+#endif
+template <bool FMA = HRT_BOX_FMA>
 HRT_LANE_FI bool box_ce(const float4& a, const float4& b, const TRay& r, float tmin, float tmax) {
   const float C[3] = {a.x, a.y, a.z}, E[3] = {b.x, b.y, b.z};
-  const float o[3] = {r.o.x, r.o.y, r.o.z}, inv[3] = {r.inv.x, r.inv.y, r.inv.z};
+  const float inv[3] = {r.inv.x, r.inv.y, r.inv.z};
   float m[3], e[3];
+  if constexpr (FMA) {
+    const float noinv[3] = {r.noinv.x, r.noinv.y, r.noinv.z}, d[3] = {r.d.x, r.d.y, r.d.z};
 #pragma unroll
-  for (int k = 0; k < 3; k++) {
-    float dc = C[k] - o[k];
+    for (int k = 0; k < 3; k++) {
+      float mk = fmaf(C[k], inv[k], noinv[k]);
 #if defined(__HIP_DEVICE_COMPILE__)
-    /* keep the three axes scalar: the SLP vectorizer would pair x and y into v_pk_* operations, which
-     * issue no faster than two scalar ones on gfx950 and cost moves (measured 4% slower) */
-    asm("" : "+v"(dc));
+      asm("" : "+v"(mk)); /* keep the axes scalar (no v_pk_*: see below) */
 #endif
-    m[k] = dc * inv[k];
-    e[k] = fabsf(dc) + E[k];
+      m[k] = mk;
+      e[k] = fmaf(fabsf(mk), fabsf(d[k]), E[k]);
+    }
+  } else {
+    const float o[3] = {r.o.x, r.o.y, r.o.z};
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      float dc = C[k] - o[k];
+#if defined(__HIP_DEVICE_COMPILE__)
+      /* keep the three axes scalar: the SLP vectorizer would pair x and y into v_pk_* operations, which
+       * issue no faster than two scalar ones on gfx950 and cost moves (measured 4% slower) */
+      asm("" : "+v"(dc));
+#endif
+      m[k] = dc * inv[k];
+      e[k] = fabsf(dc) + E[k];
+    }
   }
   /* the farthest point's distance per axis: monotone under box inclusion, so a child's inflated box
    * lies in its parent's and every hierarchy over the same leaves tests the same leaves (max |dc| +
@@ -1206,7 +1242,7 @@ HRT_LANE_FI void walk_box(const WalkSrc& src, uint32_t& i, const TRay& r, float 
 #endif
 #endif
   if constexpr (COUNT) cn.nodes++;
-  i = box_ce(a, b, r, tmin, closest) ? f2u(b.w) : skip;
+  i = box_ce<HRT_BOX_FMA && MEM != WM_HYB>(a, b, r, tmin, closest) ? f2u(b.w) : skip;
 }
 
 /* The parked leaf's primitive: the reference test on its box (aabb.rs, monotone: leaves suffice, DESIGN

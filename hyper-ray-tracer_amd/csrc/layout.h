@@ -175,7 +175,9 @@ constexpr uint32_t KIND_MASK = 0x7Fu;
  *                                                                          or ior (Dielectric); WT_GLOBAL: the
  *                                                                          texture is read from texs (any tree)
  * C, E: centre and half-extent of a box holding the node's box ([C - E, C + E] contains [mn, mx] in
- * real arithmetic: E rounded up), for the inflated test (lane.h box_ce).  Every link is explicit, so
+ * real arithmetic: E rounded up), for the inflated test (lane.h box_ce).  CE_FLOOR: max_k E_k >=
+ * 2^-12 max_k |C_k| for every box (scene.cpp box_ce_floored raises E where needed), which bounds the
+ * error box_ce's per-ray o inv product adds.  Every link is explicit, so
  * records may be placed anywhere: skip = the node that follows the subtree in pre-order (or the end
  * offset); pass = the first child for an inner node, and (payload | WALK_PEND) for a leaf: the lane
  * parks on the leaf until the wave runs its primitive test (walk_prim), which continues at the
@@ -184,8 +186,9 @@ constexpr uint32_t KIND_MASK = 0x7Fu;
  * passes) and WL_NOBOX (no reference test).
  * Placement (scene.cpp walk_place_and_write): a stream within LDS_SCENE_MAX_BYTES is laid out in
  * pre-order with each payload after its node part and staged in LDS whole; a larger one puts the node
- * parts of the hierarchy's top levels first (breadth first, up to LDS_SCENE_MAX_BYTES: the bytes the
- * kernel stages in LDS, w_hot), then everything else in pre-order in global memory. */
+ * parts a ray is likeliest to reach first (largest parent box surface first, up to LDS_SCENE_MAX_BYTES:
+ * the bytes the kernel stages in LDS, w_hot), then the other node parts in pre-order, then the payloads,
+ * in global memory. */
 constexpr uint32_t WALK_PEND = 1u << 31;
 /* the largest scene a sphere-kernel workgroup stages in LDS: two workgroups per CU share its 160 KiB,
  * each also holding a u32 result slot for each of its (at most 768) threads */

@@ -582,6 +582,32 @@ void box_ce_of(const Vec3& mn, const Vec3& mx, float* C, float* E) {
   }
 }
 
+/* layout.h CE_FLOOR: C, E of a box as box_ce_of, with max_k E_k raised to at least 2^-12 max_k |C_k| when
+ * it is smaller (only boxes far smaller than their distance from the world origin: none in the
+ * reference scenes).  fb = a float box holding [C - E, C + E] (the box itself when nothing was raised),
+ * for the enclosing nodes' boxes, so each node's inflated box still holds its children's. */
+bool box_ce_floored(const Aabb& bx, float* C, float* E, Aabb* fb) {
+  box_ce_of(bx.mn, bx.mx, C, E);
+  const float cm = std::max(std::max(fabsf(C[0]), fabsf(C[1])), fabsf(C[2]));
+  const float f = ldexpf(cm, -12); /* exact: a power-of-two scaling */
+  if (!(std::max(std::max(E[0], E[1]), E[2]) < f)) {
+    *fb = bx;
+    return false;
+  }
+  float lo[3], hi[3];
+  for (int k = 0; k < 3; k++) {
+    E[k] = std::max(E[k], f);
+    const double l = (double)C[k] - E[k], h = (double)C[k] + E[k];
+    lo[k] = (float)l;
+    if ((double)lo[k] > l) lo[k] = nextafterf(lo[k], -3.40282347e+38f);
+    hi[k] = (float)h;
+    if ((double)hi[k] < h) hi[k] = nextafterf(hi[k], 3.40282347e+38f);
+  }
+  fb->mn = v3(std::min(lo[0], bx.mn.x), std::min(lo[1], bx.mn.y), std::min(lo[2], bx.mn.z));
+  fb->mx = v3(std::max(hi[0], bx.mx.x), std::max(hi[1], bx.mx.y), std::max(hi[2], bx.mx.z));
+  return true;
+}
+
 double half_area(const Aabb& b) {
   const double x = (double)b.mx.x - b.mn.x, y = (double)b.mx.y - b.mn.y, z = (double)b.mx.z - b.mn.z;
   return x * y + y * z + z * x;
@@ -741,9 +767,9 @@ void flatten(hrt_scene* s) {
 namespace hrt {
 /* The records (layout.h): every node part at addr[i], every leaf's payload at paddr[i].  Placement:
  * if the stream fits the LDS budget, pre-order with each payload right after its leaf (the whole
- * stream is staged in LDS); otherwise the node parts of the hierarchy's top levels (breadth first,
- * up to the LDS budget) come first and are staged in LDS, the rest follows in pre-order in global
- * memory (w_hot = the staged bytes). */
+ * stream is staged in LDS); otherwise the node parts likeliest to be reached (largest parent box
+ * surface first, up to the LDS budget) come first and are staged in LDS, the other node parts follow in
+ * pre-order in global memory, then the payloads (w_hot = the staged bytes). */
 void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::vector<WalkLeaf>& leaves) {
   const uint32_t N = (uint32_t)T.size();
   uint64_t total = 0;
@@ -755,10 +781,32 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
   const bool hybrid = total > G::LDS_SCENE_MAX_BYTES && !(hot_env && strcmp(hot_env, "0") == 0);
   uint32_t off = 0;
   std::vector<char> hot(N, 0);
+  /* Hybrid placement (C4 1/8 share, r03u: +1.5% for both together, bit-identical): the node parts staged
+   * are those a ray is likeliest to reach (largest parent box surface first; HRT_WALK_HOTSEL=depth: the
+   * top levels breadth first), and the global node parts stay dense in pre-order with every payload
+   * after them (HRT_WALK_PAYLOADS=inline: each payload behind its leaf) */
+  const char* hotsel = getenv("HRT_WALK_HOTSEL");
+  const char* pl = getenv("HRT_WALK_PAYLOADS");
+  const bool by_area = !(hotsel && strcmp(hotsel, "depth") == 0);
+  const bool apart = !(pl && strcmp(pl, "inline") == 0);
   if (hybrid) {
     std::vector<uint32_t> order(N);
     for (uint32_t i = 0; i < N; i++) order[i] = i;
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return T[a].depth < T[b].depth; });
+    if (by_area) {
+      std::vector<double> key(N, 0.0);
+      key[0] = HUGE_VAL;
+      for (uint32_t i = 0; i < N; i++)
+        if (T[i].leaf < 0 && i + 1 < N) {
+          const double a = half_area(T[i].box);
+          key[i + 1] = a;
+          if (T[i + 1].end < N) key[T[i + 1].end] = a;
+        }
+      std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+        return key[a] != key[b] ? key[a] > key[b] : T[a].depth < T[b].depth;
+      });
+    } else {
+      std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return T[a].depth < T[b].depth; });
+    }
     for (uint32_t i : order) {
       if (off + G::WALK_NODE_BYTES > G::LDS_SCENE_MAX_BYTES) break;
       addr[i] = off;
@@ -772,11 +820,17 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
       addr[i] = off;
       off += G::WALK_NODE_BYTES;
     }
-    if (T[i].leaf >= 0 && !hot[i]) {
+    if (T[i].leaf >= 0 && !hot[i] && !(hybrid && apart)) {
       paddr[i] = off;
       off += PB;
     }
   }
+  if (hybrid && apart)
+    for (uint32_t i = 0; i < N; i++)
+      if (T[i].leaf >= 0 && !hot[i]) {
+        paddr[i] = off;
+        off += PB;
+      }
   for (uint32_t i = 0; i < N; i++)
     if (T[i].leaf >= 0 && hot[i]) {
       paddr[i] = off;
@@ -788,12 +842,33 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
   std::vector<float>& o = s->w_stream;
   o.assign(END / 4, 0.0f);
   const float inf = u2f(0x7f800000u);
+  /* every node's C, E (layout.h CE_FLOOR), children first: a node raised by the floor widens the boxes
+   * above it (pre-order: an inner node's children are i + 1 and T[i + 1].end) */
+  std::vector<float> CE((size_t)N * 6);
+  std::vector<Aabb> fb(N);
+  std::vector<char> fbox_ok(N, 1);
+  for (uint32_t i = N; i-- > 0;) {
+    const WNode& w = T[i];
+    float* C = &CE[(size_t)i * 6];
+    float* E = C + 3;
+    if (w.leaf >= 0 && leaves[w.leaf].nobox) {
+      C[0] = C[1] = C[2] = 0.0f;
+      E[0] = E[1] = E[2] = inf;
+      fbox_ok[i] = 0;
+      continue;
+    }
+    Aabb bx = w.box;
+    if (w.leaf < 0) { /* the union of the children's (possibly widened) boxes, when both have one */
+      const uint32_t c1 = i + 1, c2 = T[i + 1].end;
+      if (c2 < N && fbox_ok[c1] && fbox_ok[c2]) bx = box_union(bx, box_union(fb[c1], fb[c2]));
+    }
+    box_ce_floored(bx, C, E, &fb[i]);
+  }
   for (uint32_t i = 0; i < N; i++) {
     const WNode& w = T[i];
     const uint32_t skip = w.end < N ? addr[w.end] : END;
-    float C[3] = {0.0f, 0.0f, 0.0f}, E[3] = {inf, inf, inf};
-    const bool nobox = w.leaf >= 0 && leaves[w.leaf].nobox;
-    if (!nobox) box_ce_of(w.box.mn, w.box.mx, C, E);
+    const float* C = &CE[(size_t)i * 6];
+    const float* E = C + 3;
     if (w.leaf < 0) {
       need(i + 1 < N, HRT_ERR_STATE, "walk stream: inner node without children");
       put4(o, addr[i], C[0], C[1], C[2], u2f(skip));

@@ -19,19 +19,13 @@ ap.add_argument("--depth", type=int, default=50)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--ab", default="", help="comma list of flag values to alternate (A/B in one process)")
 ap.add_argument("--env", default="", help="/-list of NAME=VALUE[,NAME=VALUE] env settings to alternate (A/B)")
+ap.add_argument("--commit-env", default="", help="/-list of NAME=VALUE[,...] env settings applied while the scene is "
+                "committed (walk-stream placement knobs): one scene per setting, alternated (A/B)")
 ap.add_argument("--count", action="store_true", help="also run one instrumented pass per variant")
 ap.add_argument("--share", type=int, default=1, help="render rank 0's share of an N-way tile split (hrt/tiling.py)")
 a = ap.parse_args()
 
 _earth = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden", "earthmap_rgb8.png")
-s = hrt.preset(a.preset, 1, hrt.load_image(_earth) if os.path.exists(_earth) else None)
-s.commit(0)
-si = s.scene_info()
-print(f"scene {a.preset}: nodes {si.nodes} prims {si.prims} features {si.feature_mask:#x} cull {si.cull_mode} blob {si.blob_bytes} B", flush=True)
-cam = hrt.preset_camera(s.info, a.width, a.height)
-flag_sets = [int(x) for x in a.ab.split(",")] if a.ab else [0]
-env_sets = a.env.split("/") if a.env else [""]
-flag_sets = [(f, e) for f in flag_sets for e in env_sets]
 
 
 def set_env(e):
@@ -43,6 +37,22 @@ def set_env(e):
 def clear_env(e):
     for kv in filter(None, e.split(",")):
         os.environ.pop(kv.split("=", 1)[0], None)
+
+
+scenes = {}
+for ce in (a.commit_env.split("/") if a.commit_env else [""]):
+    set_env(ce)
+    sc = hrt.preset(a.preset, 1, hrt.load_image(_earth) if os.path.exists(_earth) else None)
+    sc.commit(0)
+    clear_env(ce)
+    scenes[ce] = sc
+    si = sc.scene_info()
+    print(f"scene {a.preset} [{ce}]: nodes {si.nodes} prims {si.prims} features {si.feature_mask:#x} cull {si.cull_mode} blob {si.blob_bytes} B", flush=True)
+s = scenes[next(iter(scenes))]
+cam = hrt.preset_camera(s.info, a.width, a.height)
+flag_sets = [int(x) for x in a.ab.split(",")] if a.ab else [0]
+env_sets = a.env.split("/") if a.env else [""]
+flag_sets = [(f, e, c) for f in flag_sets for e in env_sets for c in scenes]
 out = torch.empty((a.height, a.width, 4), dtype=torch.float32, device="cuda")
 tiles = [(0, 0, a.width, a.height)]
 if a.share > 1:
@@ -53,12 +63,12 @@ res = {k: [] for k in flag_sets}
 imgs = {}
 for r in range(a.reps):
     for key in flag_sets:
-        fl, env = key
+        fl, env, ce = key
         set_env(env)
         p = hrt.params(a.width, a.height, a.spp, a.depth, 1, tuple(s.info.background), flags=fl)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        st = hrt.render_tiles_device(s, cam, p, tiles, out.data_ptr(), 0, want_stats=True)
+        st = hrt.render_tiles_device(scenes[ce], cam, p, tiles, out.data_ptr(), 0, want_stats=True)
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         res[key].append(st.segments / dt / 1e6)
@@ -69,10 +79,10 @@ for r in range(a.reps):
 for key in flag_sets:
     print(f"{key}: median {sorted(res[key])[len(res[key])//2]:.1f} Mrays/s  identical-to-first {bool(torch.equal(imgs[key], imgs[flag_sets[0]]))}")
     if a.count:
-        fl, env = key
+        fl, env, ce = key
         set_env(env)
         p = hrt.params(a.width, a.height, a.spp, a.depth, 1, tuple(s.info.background), flags=fl | hrt.RENDER_COUNT_WORK)
-        st = hrt.render_tiles_device(s, cam, p, tiles, out.data_ptr(), 0, want_stats=True)
+        st = hrt.render_tiles_device(scenes[ce], cam, p, tiles, out.data_ptr(), 0, want_stats=True)
         clear_env(env)
         print(f"   count: nodes/ray {st.node_visits/st.segments:.2f} prims/ray {st.prim_tests/st.segments:.3f} "
               f"walk-lane-util {st.node_visits/max(1, st.walk_slots):.3f} walk-iters/ray {st.walk_slots/st.segments:.1f} "
