@@ -176,7 +176,7 @@ constexpr uint32_t KIND_MASK = 0x7Fu;
  *                                                                          texture is read from texs (any tree)
  * C, E: centre and half-extent of a box holding the node's box ([C - E, C + E] contains [mn, mx] in
  * real arithmetic: E rounded up), for the inflated test (lane.h box_ce).  CE_FLOOR: max_k E_k >=
- * 2^-12 max_k |C_k| for every box (scene.cpp box_ce_floored raises E where needed), which bounds the
+ * 2^-12 max_k |C_k| for every box (walk_box.h ce_floored raises E where needed), which bounds the
  * error box_ce's per-ray o inv product adds.  Every link is explicit, so
  * records may be placed anywhere: skip = the node that follows the subtree in pre-order (or the end
  * offset); pass = the first child for an inner node, and (payload | WALK_PEND) for a leaf: the lane

@@ -20,6 +20,7 @@
 #include <string>
 
 #include "scene_internal.h"
+#include "walk_box.h"
 
 using namespace hrt;
 using namespace hrt::host;
@@ -568,44 +569,14 @@ void build_fast(hrt_scene* s) {
  * leaves' boxes gives the reference's result.  The reference hierarchy itself is
  * kept (HRT_WALK_TREE=reference) for A/B, and whenever a leaf has no box or a box that is not a finite
  * well-formed interval. */
-/* centre / half-extent of a box, E rounded up so that [C - E, C + E] holds [mn, mx] exactly */
-void box_ce_of(const Vec3& mn, const Vec3& mx, float* C, float* E) {
-  for (int k = 0; k < 3; k++) {
-    const double lo = mn[k], hi = mx[k];
-    const float c = (float)((lo + hi) * 0.5);
-    double e = std::max((double)c - lo, hi - (double)c);
-    e += e * 0x1p-50; /* the double differences are exact unless the exponents are far apart */
-    float ef = (float)e;
-    if ((double)ef < e) ef = nextafterf(ef, 3.40282347e+38f);
-    C[k] = c;
-    E[k] = ef;
-  }
-}
-
-/* layout.h CE_FLOOR: C, E of a box as box_ce_of, with max_k E_k raised to at least 2^-12 max_k |C_k| when
- * it is smaller (only boxes far smaller than their distance from the world origin: none in the
- * reference scenes).  fb = a float box holding [C - E, C + E] (the box itself when nothing was raised),
- * for the enclosing nodes' boxes, so each node's inflated box still holds its children's. */
+/* walk_box.h ce_floored on an Aabb */
 bool box_ce_floored(const Aabb& bx, float* C, float* E, Aabb* fb) {
-  box_ce_of(bx.mn, bx.mx, C, E);
-  const float cm = std::max(std::max(fabsf(C[0]), fabsf(C[1])), fabsf(C[2]));
-  const float f = ldexpf(cm, -12); /* exact: a power-of-two scaling */
-  if (!(std::max(std::max(E[0], E[1]), E[2]) < f)) {
-    *fb = bx;
-    return false;
-  }
-  float lo[3], hi[3];
-  for (int k = 0; k < 3; k++) {
-    E[k] = std::max(E[k], f);
-    const double l = (double)C[k] - E[k], h = (double)C[k] + E[k];
-    lo[k] = (float)l;
-    if ((double)lo[k] > l) lo[k] = nextafterf(lo[k], -3.40282347e+38f);
-    hi[k] = (float)h;
-    if ((double)hi[k] < h) hi[k] = nextafterf(hi[k], 3.40282347e+38f);
-  }
-  fb->mn = v3(std::min(lo[0], bx.mn.x), std::min(lo[1], bx.mn.y), std::min(lo[2], bx.mn.z));
-  fb->mx = v3(std::max(hi[0], bx.mx.x), std::max(hi[1], bx.mx.y), std::max(hi[2], bx.mx.z));
-  return true;
+  const float mn[3] = {bx.mn.x, bx.mn.y, bx.mn.z}, mx[3] = {bx.mx.x, bx.mx.y, bx.mx.z};
+  float fmn[3], fmx[3];
+  const bool raised = walkbox::ce_floored(mn, mx, C, E, fmn, fmx);
+  fb->mn = v3(fmn[0], fmn[1], fmn[2]);
+  fb->mx = v3(fmx[0], fmx[1], fmx[2]);
+  return raised;
 }
 
 double half_area(const Aabb& b) {

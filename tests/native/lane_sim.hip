@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "lane.h"
+#include "walk_box.h"
 
 using namespace hrt;
 using namespace hrt::lane;
@@ -219,6 +220,44 @@ int lane_sim_render(const void* blob, const hrt_blob_info* bi, const hrt_camera*
         else render_pixel<G::CULL_REFERENCE, 2>(P, x0 + x, y0 + y, o, cnt);
       }
     }
+  return 0;
+}
+
+
+/* The culling property behind CULL_EXACT on single spheres: whenever the reference's
+ * sphere test (sphere.rs:38-55, lane.h sphere_root_at) accepts a root in [tmin, tmax], the walk's inflated
+ * test (lane.h box_ce, both forms) on the sphere's box as the stream builder encodes it (walk_box.h
+ * ce_floored over sphere.rs's bounding box) must pass.  sph: n x (cx, cy, cz, r); rays: m x (o, d).
+ * cnt: [pairs accepted, accepted outside the sphere's box (grazing false hits), culled by the fused form,
+ * culled by the sub/mul/add form, boxes raised by the floor, rays in NaN mode] */
+int lane_sim_cull_property(const float* sph, uint32_t n_sph, const float* rays, uint32_t n_rays, float tmin,
+                           float tmax, uint64_t* cnt) {
+  for (uint32_t q = 0; q < n_rays; q++) {
+    TRay r;
+    set_dir(r, v3(rays[6 * q], rays[6 * q + 1], rays[6 * q + 2]), v3(rays[6 * q + 3], rays[6 * q + 4], rays[6 * q + 5]));
+    if (r.noinv.x != r.noinv.x) cnt[5]++;
+  }
+  for (uint32_t i = 0; i < n_sph; i++) {
+    const Vec3 c = v3(sph[4 * i], sph[4 * i + 1], sph[4 * i + 2]);
+    const float rad = sph[4 * i + 3];
+    const Vec3 rv = v3(rad, rad, rad);
+    const Vec3 bmn = c - rv, bmx = c + rv; /* sphere.rs bounding_box */
+    const float mn[3] = {bmn.x, bmn.y, bmn.z}, mx[3] = {bmx.x, bmx.y, bmx.z};
+    float C[3], E[3], fmn[3], fmx[3];
+    if (walkbox::ce_floored(mn, mx, C, E, fmn, fmx)) cnt[4]++;
+    const float4 a = make_float4(C[0], C[1], C[2], 0.0f), b = make_float4(E[0], E[1], E[2], 0.0f);
+    for (uint32_t q = 0; q < n_rays; q++) {
+      TRay r;
+      set_dir(r, v3(rays[6 * q], rays[6 * q + 1], rays[6 * q + 2]), v3(rays[6 * q + 3], rays[6 * q + 4], rays[6 * q + 5]));
+      float t;
+      if (!sphere_root_at(c, rad, r, tmin, tmax, t)) continue;
+      cnt[0]++;
+      const Vec3 p = r.o + t * r.d;
+      if (p.x < mn[0] || p.x > mx[0] || p.y < mn[1] || p.y > mx[1] || p.z < mn[2] || p.z > mx[2]) cnt[1]++;
+      if (!box_ce<true>(a, b, r, tmin, tmax)) cnt[2]++;
+      if (!box_ce<false>(a, b, r, tmin, tmax)) cnt[3]++;
+    }
+  }
   return 0;
 }
 

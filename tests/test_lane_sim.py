@@ -266,3 +266,49 @@ def test_sample_chunks_of_the_headline_frame(sim):
     """C2 (500 spp, sphere class): 30 head chunks (6, then 29 of 16) and the tail 8, 8, 4, 4, 2, 2, 1, 1."""
     sizes = [b - a for a, b in _chunks(sim, 500, 0)]
     assert sizes == [6] + [16] * 29 + [8, 8, 4, 4, 2, 2, 1, 1]
+
+
+def _cull_rays(rng, c, r, n):
+    """Rays aimed at grazing points of the sphere (c, r): origins from inside its box to 1e4 radii away,
+    targets on the surface jittered by 1e-8 .. 1 radius, directions of any scale, some axis-aligned."""
+    u = rng.normal(size=(n, 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    w = rng.normal(size=(n, 3))
+    w -= (w * u).sum(axis=1, keepdims=True) * u
+    w /= np.maximum(np.linalg.norm(w, axis=1, keepdims=True), 1e-30)
+    target = c + r * u + (r * 10.0 ** rng.uniform(-8, 0, size=(n, 1))) * w * rng.choice([-1.0, 1.0], size=(n, 1))
+    v = rng.normal(size=(n, 3))
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    o = c + v * (r * 10.0 ** rng.uniform(-0.5, 4, size=(n, 1)))
+    d = (target - o) * 10.0 ** rng.uniform(-3, 3, size=(n, 1))
+    axis = rng.random(n) < 0.1  # zero components: rays that set_dir puts in NaN mode
+    d[axis, rng.integers(0, 3, size=int(axis.sum()))] = 0.0
+    return np.concatenate([o, d], axis=1).astype(np.float32)
+
+
+def test_exact_culling_property_on_grazing_rays(sim):
+    """the walk's inflated box test never culls a sphere whose reference test accepts a
+    root, including grazing false hits outside the sphere's box (G18), tiny spheres far from the origin
+    (the CE_FLOOR bound of the fused o*inv form) and rays with zero direction components (NaN mode)."""
+    rng = np.random.default_rng(7)
+    spheres = []
+    for _ in range(60):  # tiny spheres far from the world origin: the floor raises their boxes
+        spheres.append((*rng.uniform(-5000, 5000, 3), 10.0 ** rng.uniform(-6, -2)))
+    for _ in range(60):  # scene-sized spheres
+        spheres.append((*rng.uniform(-50, 50, 3), 10.0 ** rng.uniform(-1, 1)))
+    spheres += [(0.0, -1000.0, 0.0, 1000.0), (0.0, 0.0, 0.0, 5000.0), (4.0, 1.0, 0.0, 1.0)]
+    fn = sim.lane_sim_cull_property
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_float, ctypes.c_float,
+                   ctypes.c_void_p]
+    total = np.zeros(6, np.uint64)
+    for s in spheres:
+        sph = np.array(s, np.float32)
+        rays = _cull_rays(rng, sph[:3].astype(np.float64), float(sph[3]), 4000)
+        cnt = np.zeros(6, np.uint64)
+        assert fn(sph.ctypes.data, 1, rays.ctypes.data, len(rays), 0.001, float("inf"), cnt.ctypes.data) == 0
+        assert cnt[2] == 0 and cnt[3] == 0, (s, cnt)
+        total += cnt
+    accepted, outside, _, _, raised, nan_rays = (int(x) for x in total)
+    print("cull property totals", total)
+    assert accepted > 100000 and outside > 0  # grazing false hits were produced and none was culled
+    assert raised >= 60 and nan_rays > 0
