@@ -162,7 +162,8 @@ struct TRay {
   float time;
   float dd;  /* dot(d, d): sphere.rs:42 `a`, constant for the ray */
   float rdd; /* RN(1 / dd) for div_rn, or NaN when dd is outside div_rn's fast domain */
-  float tau; /* (time - time0) / (time1 - time0) of the scene's moving spheres (uniform motion only) */
+  float tau; /* (time - time0) / (time1 - time0) of the scene's moving spheres under uniform motion, else the
+               time itself: the walks read only this field (one register for both) */
 };
 
 /* x / r.dd correctly rounded (bit-identical to IEEE division) by a 3-instruction core: with
@@ -218,7 +219,7 @@ HRT_LANE_FI void set_dir(TRay& r, Vec3 o, Vec3 d) {
 HRT_LANE_FI void set_time(TRay& r, float time, const KParams& P) {
   r.time = time;
   /* moving_sphere.rs:55-58: identical for every moving sphere when they share time0/time1 */
-  r.tau = P.motion_uniform ? (time - P.motion_t0) / P.motion_span : 0.0f;
+  r.tau = P.motion_uniform ? (time - P.motion_t0) / P.motion_span : time;
 }
 
 HRT_LANE_FI void set_ray(TRay& r, Vec3 o, Vec3 d, float time, const KParams& P) {
@@ -373,7 +374,7 @@ HRT_LANE_FI bool sphere_root(const G::Prim* pp, uint32_t kind, const TRay& r, fl
   Vec3 c = v3(p0.x, p0.y, p0.z);
   if (kind == G::P_MOVING) {
     float4 p1 = ld4(pp->p1);
-    const float f = motion_uniform ? r.tau : (r.time - p1.w) / pp->p2[0];
+    const float f = motion_uniform ? r.tau : (r.tau - p1.w) / pp->p2[0]; /* r.tau: the time (TRay) */
     c = c + f * v3(p1.x, p1.y, p1.z);
   }
   return sphere_root_at(c, p0.w, r, tmin, tmax, root);
@@ -1178,9 +1179,11 @@ HRT_LANE_FI void basic_step(const KParams& P, const G::Node* __restrict__ nodes,
  * computation stay below ~2.6e-4 D' |inv_k|, inside the slack of EXACT_MARGIN (layout.h: 4e-3 covers the
  * 2.4e-3 needed with 1.6e-3 to spare).  A NaN bound (the old form: inv_k = +-inf with C_k = o_k or
  * E_k = 0) is ignored by max3/min3: no constraint; a ray whose noinv is NaN (set_dir) passes every box.
- * An infinite box (E = +inf) always passes.  The hybrid LDS / global walk (WM_HYB, latency-bound) keeps
- * the sub/mul/add form: the three more live registers cost it 4.5% (C4 1/8 share), while the LDS walks
- * gain 1.5% (C2) from the two fewer instructions per axis. */
+ * An infinite box (E = +inf) always passes.  The hybrid LDS / global walk (WM_HYB, latency-bound) and the
+ * sphere kernel's HEAVY instantiation keep the sub/mul/add form: the three more live registers cost them
+ * 4.5% (C4 1/8 share) and 3% (C3), while the LDS walks gain 1.5-2% (C2: 14473 -> 14785 Mrays/s on the
+ * r03v bench) from the two fewer instructions per axis.  tests/test_lane_sim.py checks both forms on
+ * grazing, tiny-far and axis-aligned rays. */
 #ifndef HRT_BOX_FMA
 #define HRT_BOX_FMA 1
 #endif
@@ -1231,7 +1234,9 @@ HRT_LANE_FI bool box_ce(const float4& a, const float4& b, const TRay& r, float t
 }
 
 /* One node step: an inner node moves to pass / skip; a passed leaf parks the lane on it (WALK_PEND). */
-template <bool COUNT, int MEM>
+/* FMA: box_ce's fused form (default except for the latency-bound hybrid walk; the sphere kernel's
+ * HEAVY instantiation passes false: at its 128-VGPR cap the three more live registers cost 3% on C3) */
+template <bool COUNT, int MEM, bool FMA = HRT_BOX_FMA && MEM != WM_HYB>
 HRT_LANE_FI void walk_box(const WalkSrc& src, uint32_t& i, const TRay& r, float tmin, float closest, Counts& cn) {
   const float4 a = wload<MEM>(src, i), b = wload<MEM>(src, i + 16u);
   uint32_t skip = f2u(a.w);
@@ -1242,7 +1247,7 @@ HRT_LANE_FI void walk_box(const WalkSrc& src, uint32_t& i, const TRay& r, float 
 #endif
 #endif
   if constexpr (COUNT) cn.nodes++;
-  i = box_ce<HRT_BOX_FMA && MEM != WM_HYB>(a, b, r, tmin, closest) ? f2u(b.w) : skip;
+  i = box_ce<FMA>(a, b, r, tmin, closest) ? f2u(b.w) : skip;
 }
 
 /* The parked leaf's primitive: the reference test on its box (aabb.rs, monotone: leaves suffice, DESIGN
@@ -1258,7 +1263,7 @@ HRT_LANE_FI void walk_leaf_test(const KParams& P, const WalkSrc& src, uint32_t l
   Vec3 c = v3(s0.x, s0.y, s0.z);
   if (w & G::WL_MOVING) { /* moving_sphere.rs:55-58 */
     const float4 s1 = wload<MEM>(src, leaf + 48u);
-    const float f = P.motion_uniform ? r.tau : (r.time - s0.w) / s1.w;
+    const float f = P.motion_uniform ? r.tau : (r.tau - s0.w) / s1.w; /* r.tau: the time (TRay) */
     c = c + f * v3(s1.x, s1.y, s1.z);
   }
   float t;

@@ -197,7 +197,10 @@ void render_gwalk_kernel(KParams P) {
       bool done = true;
       if (traced) {
         ps.pk.segment++;
-        done = shade<true, COUNT, TRIM>(Q, ps, winner, closest, r.o, r.d, r.time, r.tau, cn) || ps.depth_left == 0;
+        /* without media nothing but the motion factor reads the ray's time: r.tau holds it (lane.h TRay),
+         * so r.time is dead in the media-free instantiations (one register fewer) */
+        done = shade<true, COUNT, TRIM>(Q, ps, winner, closest, r.o, r.d, MEDIA ? r.time : r.tau, r.tau, cn) ||
+               ps.depth_left == 0;
       }
       if (done) {
         walking = false;

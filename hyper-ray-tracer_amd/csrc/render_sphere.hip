@@ -145,7 +145,7 @@ void render_basic_kernel(KParams P) {
       for (int u = 0; u < WALK_UNROLL; u++) {
         if constexpr (COUNT) cn.walk_slots++;
         if (node < end) {
-          if constexpr (WS) walk_box<COUNT, WMEM>(ws, node, r, tmin_c, closest, cn);
+          if constexpr (WS) walk_box<COUNT, WMEM, HRT_BOX_FMA && WMEM != WM_HYB && !HEAVY>(ws, node, r, tmin_c, closest, cn);
           else basic_box<CULL, COUNT, STRIDE>(P, nodes, node, r, closest, cn);
         } else if constexpr (COUNT) {
           if (walk_pending(node)) cn.park_slots++;
@@ -204,8 +204,8 @@ void render_basic_kernel(KParams P) {
     if (shading) {
       bool done = true;
       if (traced) {
-        if constexpr (WS) done = shade_walk<COUNT, WMEM, HEAVY>(Q, ws, ps, winner, closest, r.o, r.d, r.time, r.tau, sum, cn);
-        else done = shade<false, COUNT>(P, ps, winner, closest, r.o, r.d, r.time, r.tau, cn);
+        if constexpr (WS) done = shade_walk<COUNT, WMEM, HEAVY>(Q, ws, ps, winner, closest, r.o, r.d, r.tau, r.tau, sum, cn);
+        else done = shade<false, COUNT>(P, ps, winner, closest, r.o, r.d, r.tau, r.tau, cn); /* time = r.tau unless uniform (TRay) */
         done = done || ps.depth_left == 0;
       }
       if (done) {
