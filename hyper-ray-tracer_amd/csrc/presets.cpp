@@ -66,6 +66,47 @@ HittableP generate_random_scene(Ctx& c, int n) {
   return mk<BvhNode>(std::move(objects), 0.0f, 1.0f);
 }
 
+/* build-defined: the random scene's grid with every sphere moving over its OWN shutter interval
+ * (moving_sphere.rs:53-58 divides by each sphere's time1 - time0), so the kernels' scene-wide motion
+ * factor does not apply; oracle.cpp preset 12 draws the same numbers in the same order */
+HittableP generate_motion(Ctx& c) {
+  std::vector<HittableP> objects;
+  objects.push_back(mk<Sphere>(v3(0.0f, -1000.0f, 0.0f), 1000.0f,
+                               lambert(std::make_shared<CheckerTexture>(solid(0.2f, 0.3f, 0.1f),
+                                                                        solid(0.9f, 0.9f, 0.9f)))));
+  Rng& rand = c.rand;
+  for (int a = -4; a < 4; a++) {
+    for (int b = -4; b < 4; b++) {
+      const float choose_material = rand.gen_f32();
+      const float cx = (float)a + 0.9f * rand.gen_f32();
+      const float cz = (float)b + 0.9f * rand.gen_f32();
+      const Vec3 center = v3(cx, 0.2f, cz);
+      const float t0 = rand.gen_range_f32(-0.5f, 0.5f);
+      const float t1 = t0 + rand.gen_range_f32(0.25f, 1.5f);
+      const float dx = rand.gen_range_f32(-0.3f, 0.3f), dy = rand.gen_range_f32(0.0f, 0.5f),
+                  dz = rand.gen_range_f32(-0.3f, 0.3f);
+      const Vec3 center_2 = center + v3(dx, dy, dz);
+      MaterialP m;
+      if (choose_material < 0.6f) {
+        const float r = rand.gen_f32(), g = rand.gen_f32(), bl = rand.gen_f32();
+        m = lambert(solid(r, g, bl));
+      } else if (choose_material < 0.85f) {
+        const float r = rand.gen_range_f32(0.5f, 1.0f), g = rand.gen_range_f32(0.5f, 1.0f),
+                    bl = rand.gen_range_f32(0.5f, 1.0f);
+        const float fuzz = rand.gen_range_f32(0.0f, 0.5f);
+        m = std::make_shared<Metal>(v3(r, g, bl), fuzz);
+      } else {
+        m = std::make_shared<Dielectric>(1.5f);
+      }
+      objects.push_back(mk<MovingSphere>(center, center_2, t0, t1, 0.2f, m));
+    }
+  }
+  objects.push_back(mk<Sphere>(v3(0.0f, 1.0f, 0.0f), 1.0f, std::make_shared<Dielectric>(1.5f)));
+  objects.push_back(mk<MovingSphere>(v3(-4.0f, 1.0f, 0.0f), v3(-4.0f, 1.5f, 0.0f), 0.0f, 2.0f, 1.0f,
+                                     lambert(solid(0.4f, 0.2f, 0.1f))));
+  return mk<BvhNode>(std::move(objects), 0.0f, 1.0f);
+}
+
 /* :567-587 */
 HittableP generate_two_spheres() {
   MaterialP checker =
@@ -266,6 +307,7 @@ extern "C" hrt_status hrt_preset_build(hrt_scene* s, int32_t preset, uint64_t sc
       case HRT_PRESET_RANDOM: info->aperture = 0.1f; world = generate_random_scene(c, 11); break;
       case HRT_PRESET_RANDOM_10K: info->aperture = 0.1f; world = generate_random_scene(c, 50); break;
       case HRT_PRESET_RANDOM_40K: info->aperture = 0.1f; world = generate_random_scene(c, 100); break;
+      case HRT_PRESET_MOTION: info->aperture = 0.05f; world = generate_motion(c); break;
       case HRT_PRESET_TWO_SPHERES: world = generate_two_spheres(); break;
       case HRT_PRESET_TWO_PERLIN_SPHERES: world = generate_two_perlin_spheres(c); break;
       case HRT_PRESET_EARTH: world = generate_earth(c); break;

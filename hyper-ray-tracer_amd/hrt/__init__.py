@@ -39,6 +39,7 @@ PRESETS = {
     "random_10k": 9,
     "features": 10,
     "random_40k": 11,  # build-defined: 39.9k leaves, the device-built walk hierarchy by default
+    "motion": 12,  # build-defined: moving spheres with their own shutter intervals (no scene-wide factor)
 }
 
 

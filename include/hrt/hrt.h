@@ -148,7 +148,9 @@ enum {
   HRT_PRESET_FEATURES = 10,          /* X/Z rotations, lists, nested instances, media in instances */
   HRT_PRESET_RANDOM_40K = 11,        /* :511-545 with a, b in [-100, 100): 39.9k leaves, so the walk stream's
                                         hierarchy is built on the device by default */
-  HRT_PRESET_COUNT = 12
+  HRT_PRESET_MOTION = 12,            /* moving spheres with their own shutter intervals (moving_sphere.rs:53-58
+                                        per sphere: no scene-wide motion factor), a sphere-kernel scene */
+  HRT_PRESET_COUNT = 13
 };
 
 const char* hrt_last_error(void);

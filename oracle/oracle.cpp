@@ -860,6 +860,46 @@ static HitP random_scene(Builder& B, int n) {
   return HitP(new BvhNode(std::move(objects), 0.0f, 1.0f));
 }
 
+/* build-defined (library presets.cpp generate_motion): moving spheres with their own shutter intervals,
+ * drawn in the library's order; moving_sphere.rs:53-58 per sphere */
+static HitP motion_scene(Builder& B) {
+  std::vector<HitP> objects;
+  objects.emplace_back(new Sphere(v3(0.0f, -1000.0f, 0.0f), 1000.0f,
+                                  lambert(std::make_shared<CheckerTexture>(solid(0.2f, 0.3f, 0.1f),
+                                                                           solid(0.9f, 0.9f, 0.9f)))));
+  Rng& rand = B.rand;
+  for (int a = -4; a < 4; a++) {
+    for (int b = -4; b < 4; b++) {
+      const float choose_material = rand.gen_f32();
+      const float cx = (float)a + 0.9f * rand.gen_f32();
+      const float cz = (float)b + 0.9f * rand.gen_f32();
+      const Vec3 center = v3(cx, 0.2f, cz);
+      const float t0 = rand.gen_range_f32(-0.5f, 0.5f);
+      const float t1 = t0 + rand.gen_range_f32(0.25f, 1.5f);
+      const float dx = rand.gen_range_f32(-0.3f, 0.3f), dy = rand.gen_range_f32(0.0f, 0.5f),
+                  dz = rand.gen_range_f32(-0.3f, 0.3f);
+      const Vec3 center_2 = center + v3(dx, dy, dz);
+      MatP m;
+      if (choose_material < 0.6f) {
+        const float r = rand.gen_f32(), g = rand.gen_f32(), bl = rand.gen_f32();
+        m = lambert(solid(r, g, bl));
+      } else if (choose_material < 0.85f) {
+        const float r = rand.gen_range_f32(0.5f, 1.0f), g = rand.gen_range_f32(0.5f, 1.0f),
+                    bl = rand.gen_range_f32(0.5f, 1.0f);
+        const float fuzz = rand.gen_range_f32(0.0f, 0.5f);
+        m = std::make_shared<Metal>(v3(r, g, bl), fuzz);
+      } else {
+        m = std::make_shared<Dielectric>(1.5f);
+      }
+      objects.emplace_back(new MovingSphere(center, center_2, t0, t1, 0.2f, m));
+    }
+  }
+  objects.emplace_back(new Sphere(v3(0.0f, 1.0f, 0.0f), 1.0f, std::make_shared<Dielectric>(1.5f)));
+  objects.emplace_back(new MovingSphere(v3(-4.0f, 1.0f, 0.0f), v3(-4.0f, 1.5f, 0.0f), 0.0f, 2.0f, 1.0f,
+                                        lambert(solid(0.4f, 0.2f, 0.1f))));
+  return HitP(new BvhNode(std::move(objects), 0.0f, 1.0f));
+}
+
 static void cornell_walls(std::vector<HitP>& objects, MatP& white) {
   MatP red = lambert(solid(0.65f, 0.05f, 0.05f));
   white = lambert(solid(0.73f, 0.73f, 0.73f));
@@ -894,6 +934,10 @@ static Scene* build_preset(int preset, uint64_t seed, const uint8_t* img, uint32
     case 9: /* config 4: 10k spheres */
       I.aperture = 0.1f;
       sc->world = random_scene(B, 50);
+      break;
+    case 12: /* moving spheres with their own shutter intervals */
+      I.aperture = 0.05f;
+      sc->world = motion_scene(B);
       break;
     case 11: /* 40k spheres (a device-built walk hierarchy in the library) */
       I.aperture = 0.1f;

@@ -29,6 +29,7 @@ CASES = [
     ("earth_perlin", 48, 27, 16, 50),
     ("random_10k", 48, 27, 4, 50),
     ("features", 64, 36, 16, 50),
+    ("motion", 64, 36, 16, 50),          # per-sphere shutter intervals: no scene-wide motion factor
 ]
 
 

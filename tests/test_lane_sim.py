@@ -27,7 +27,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 TOL = 1e-3
 CULL_REFERENCE, CULL_SLAB, CULL_EXACT = 0, 1, 2
-BASIC_SCENES = {"random", "two_spheres", "random_10k"}
+BASIC_SCENES = {"random", "two_spheres", "random_10k", "motion"}
 # sphere scenes with noise / image textures: the sphere kernel's HEAVY instantiation (layout.h F_HEAVY_TEX)
 HEAVY_SPHERE_SCENES = {"earth", "two_perlin_spheres", "earth_perlin"}
 
@@ -79,6 +79,7 @@ CASES = [
     ("earth_perlin", 48, 27, 8, 50),
     ("random_10k", 32, 18, 2, 50),
     ("features", 48, 27, 8, 50),
+    ("motion", 48, 27, 8, 50),           # moving spheres with their own shutter intervals (TRay.tau = time)
     ("cornell", 24, 24, 4, 2),           # depth cap
     ("cornell", 12, 12, 70, 50),         # general scene: three chunks of >= 32 samples (lane.h sample_chunk)
     ("final", 8, 8, 40, 50),             # deep general scene (> 1024 nodes): three chunks of >= 16
