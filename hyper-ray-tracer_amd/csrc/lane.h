@@ -1285,6 +1285,44 @@ HRT_LANE_FI void walk_prim(const KParams& P, const WalkSrc& src, uint32_t& i, co
   walk_leaf_test<COUNT, MEM>(P, src, leaf, r, closest, winner, cn);
 }
 
+/* A one-node program (layout.h GL_ONE): trace_ray's body for a K_BOX_PRIM or K_PRIM node at i -- the
+ * node's CULL_EXACT box test, then its rect or sphere against closest -- without the node loop and the
+ * dispatch over every kind, whose code the wave otherwise runs for any lane that needs it. */
+#ifndef HRT_GWALK_ONE
+#define HRT_GWALK_ONE 1
+#endif
+template <bool COUNT>
+HRT_LANE_FI void gwalk_one(const KParams& P, const G::Node* __restrict__ nodes, const G::Prim* __restrict__ prims,
+                           uint32_t i, const TRay& r, float tmin, float& closest, uint32_t& winner, Counts& cn) {
+  const G::Node* np = nodes + i;
+  const float4 a = ld4(np->mn);
+  const float4 b = ld4(np->mx);
+  const uint32_t kp = f2u(b.w);
+  if constexpr (COUNT) cn.nodes++;
+  if (((kp >> 24) & G::KIND_MASK) == G::K_BOX_PRIM &&
+      !box_hit<G::CULL_EXACT>(a, b, r, tmin, closest, (kp & G::NODE_REF_ONLY) != 0))
+    return;
+  const G::Prim* pp = prims + (kp & 0xFFFFFFu);
+  const uint32_t km = pp->km;
+  if constexpr (COUNT) cn.prims++;
+  float t;
+  bool h;
+  if ((km & 3u) == G::P_RECT) h = rect_t(pp, (km >> 2) & 3u, r, tmin, closest, t);
+  else h = sphere_root(pp, km & 3u, r, tmin, closest, t, P.motion_uniform != 0);
+  if (h) {
+    closest = t;
+    winner = i;
+  }
+}
+
+template <bool MEDIA, bool COUNT>
+HRT_LANE_FI void gwalk_program(const KParams& P, const G::Node* __restrict__ nodes, const G::Prim* __restrict__ prims,
+                               uint32_t flags, uint32_t begin, uint32_t end, const TRay& r, float& closest,
+                               uint32_t& winner, const PathKey& pk, Counts& cn) {
+  if (HRT_GWALK_ONE && (flags & G::GL_ONE)) gwalk_one<COUNT>(P, nodes, prims, begin, r, P.t_min, closest, winner, cn);
+  else trace_ray<G::CULL_EXACT, true, MEDIA, COUNT>(P, nodes, prims, begin, end, r, P.t_min, closest, winner, pk, cn);
+}
+
 /* A passed leaf of the GENERAL walk stream (layout.h): the reference test of the enclosing BvhNode box
  * (box-less leaves, GL_BOX), then the leaf's program -- its range of the reference stream, whose first
  * node is the leaf's own box (the reference test at the leaf) -- from the world ray
@@ -1295,32 +1333,29 @@ HRT_LANE_FI void gwalk_leaf_test(const KParams& P, const G::Node* __restrict__ n
                                  uint32_t& gstate, const PathKey& pk, Counts& cn) {
   const float4 h = wload<MEM>(src, leaf);
   const uint32_t flags = f2u(h.z);
-  if (!(flags & (G::GL_BOX | G::GL_INST))) {
-    trace_ray<G::CULL_EXACT, true, MEDIA, COUNT>(P, nodes, prims, f2u(h.x), f2u(h.y), r, P.t_min, closest, winner, pk, cn);
-    return;
-  }
-  const float4 bmn = wload<MEM>(src, leaf + 16u);
-  if (flags & G::GL_BOX) { /* the group's box: tested at the group's first leaf, the outcome kept (layout.h) */
-    const float4 bmx = wload<MEM>(src, leaf + 32u);
-    const uint32_t g = f2u(bmx.w);
-    if ((gstate & 0x7FFFFFFFu) != g) gstate = g | (box_ref(bmn, bmx, r, P.t_min, closest) ? 0x80000000u : 0u);
-    if (!(gstate >> 31)) return;
-  }
-  if (!(flags & G::GL_INST)) {
-    trace_ray<G::CULL_EXACT, true, MEDIA, COUNT>(P, nodes, prims, f2u(h.x), f2u(h.y), r, P.t_min, closest, winner, pk, cn);
-    return;
-  }
-  /* a leaf of a flattened instance chain (layout.h GL_INST): the ray in the innermost instance's frame,
-   * as the reference's Translation / Rotation hits hand it down (apply_chain), with 1/d and d.d of the
-   * turned direction where the program reads them */
+  /* one call site for the program (the ray: the world ray, or the innermost instance frame's) */
   TRay lr = r;
-  apply_chain(P, f2u(bmn.w), lr.o, lr.d);
-  if (flags & G::GL_INV) lr.inv = v3(1.0f / lr.d.x, 1.0f / lr.d.y, 1.0f / lr.d.z);
-  if (flags & G::GL_DD) {
-    lr.dd = dot(lr.d, lr.d);
-    lr.rdd = div_rn_y(lr.dd);
+  if (flags & (G::GL_BOX | G::GL_INST)) {
+    const float4 bmn = wload<MEM>(src, leaf + 16u);
+    if (flags & G::GL_BOX) { /* the group's box: tested at the group's first leaf, the outcome kept (layout.h) */
+      const float4 bmx = wload<MEM>(src, leaf + 32u);
+      const uint32_t g = f2u(bmx.w);
+      if ((gstate & 0x7FFFFFFFu) != g) gstate = g | (box_ref(bmn, bmx, r, P.t_min, closest) ? 0x80000000u : 0u);
+      if (!(gstate >> 31)) return;
+    }
+    if (flags & G::GL_INST) {
+      /* a leaf of a flattened instance chain (layout.h GL_INST): the ray in the innermost instance's frame,
+       * as the reference's Translation / Rotation hits hand it down (apply_chain), with 1/d and d.d of the
+       * turned direction where the program reads them */
+      apply_chain(P, f2u(bmn.w), lr.o, lr.d);
+      if (flags & G::GL_INV) lr.inv = v3(1.0f / lr.d.x, 1.0f / lr.d.y, 1.0f / lr.d.z);
+      if (flags & G::GL_DD) {
+        lr.dd = dot(lr.d, lr.d);
+        lr.rdd = div_rn_y(lr.dd);
+      }
+    }
   }
-  trace_ray<G::CULL_EXACT, true, MEDIA, COUNT>(P, nodes, prims, f2u(h.x), f2u(h.y), lr, P.t_min, closest, winner, pk, cn);
+  gwalk_program<MEDIA, COUNT>(P, nodes, prims, flags, f2u(h.x), f2u(h.y), lr, closest, winner, pk, cn);
 }
 
 template <bool MEDIA, bool COUNT, int MEM>

@@ -227,6 +227,9 @@ constexpr uint32_t GWALK_PAYLOAD_BYTES = 48;
  * below) recomputed when the chain turns the direction (GL_DIR).  Its GL_BOX box is then the nearest
  * world-frame BvhNode box around the chain; boxes inside the instance are tested by the program itself. */
 constexpr uint32_t GL_BOX = 1u, GL_INST = 2u, GL_DIR = 4u, GL_INV = 8u, GL_DD = 16u;
+/* GL_ONE: the program is ONE primitive node (K_BOX_PRIM or K_PRIM: a BvhNode leaf, a Cuboid side, a List
+ * member), run without trace_ray's node loop and kind dispatch (lane.h gwalk_one) */
+constexpr uint32_t GL_ONE = 32u;
 
 }  // namespace gpu
 }  // namespace hrt

@@ -851,7 +851,12 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
     put4(o, addr[i] + 16, E[0], E[1], E[2], u2f(paddr[i] | G::WALK_PEND));
     if (s->w_general) { /* layout.h general-scene walk stream: the leaf's program range */
       const uint32_t q = paddr[i];
-      put4(o, q, u2f(L.begin), u2f(L.end), u2f((L.has_rbox ? G::GL_BOX : 0u) | L.gflags), u2f(skip << 2));
+      uint32_t one = 0;
+      if (L.end == L.begin + 1) {
+        const uint32_t k = (s->g_nodes[L.begin].kp >> 24) & G::KIND_MASK;
+        if (k == G::K_BOX_PRIM || k == G::K_PRIM) one = G::GL_ONE;
+      }
+      put4(o, q, u2f(L.begin), u2f(L.end), u2f((L.has_rbox ? G::GL_BOX : 0u) | L.gflags | one), u2f(skip << 2));
       put4(o, q + 16, L.rbox.mn.x, L.rbox.mn.y, L.rbox.mn.z, u2f(L.inst));
       put4(o, q + 32, L.rbox.mx.x, L.rbox.mx.y, L.rbox.mx.z, u2f(L.rgroup));
       continue;

@@ -10,7 +10,7 @@ pat = sys.argv[1] if len(sys.argv) > 1 else "render_basic_kernelILi2ELb0ELb1E"
 extra = sys.argv[2:]
 out = "/tmp/walk_isa.s"
 sphere = "basic" in pat  # render_basic_kernel lives in render_sphere.hip, built without SLP (Makefile)
-src = os.path.join(ROOT, "hyper-ray-tracer_amd", "csrc", "render_sphere.hip" if sphere else "render.hip")
+src = os.path.join(ROOT, "hyper-ray-tracer_amd", "csrc", "render_sphere.hip" if sphere else ("render_general.hip" if "gwalk" in pat else "render.hip"))
 subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
                 "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "hyper-ray-tracer_amd", "csrc"),
                 "--offload-arch=gfx950", "--cuda-device-only", "-S", src, "-o", out]
