@@ -1187,6 +1187,9 @@ HRT_LANE_FI void basic_step(const KParams& P, const G::Node* __restrict__ nodes,
 #ifndef HRT_BOX_FMA
 #define HRT_BOX_FMA 1
 #endif
+#ifndef HRT_BOX_FMA_ALL
+#define HRT_BOX_FMA_ALL 0 /* 1: the hybrid walk and HEAVY use the fused form too */
+#endif
 template <bool FMA = HRT_BOX_FMA>
 HRT_LANE_FI bool box_ce(const float4& a, const float4& b, const TRay& r, float tmin, float tmax) {
   const float C[3] = {a.x, a.y, a.z}, E[3] = {b.x, b.y, b.z};
@@ -1236,7 +1239,7 @@ HRT_LANE_FI bool box_ce(const float4& a, const float4& b, const TRay& r, float t
 /* One node step: an inner node moves to pass / skip; a passed leaf parks the lane on it (WALK_PEND). */
 /* FMA: box_ce's fused form (default except for the latency-bound hybrid walk; the sphere kernel's
  * HEAVY instantiation passes false: at its 128-VGPR cap the three more live registers cost 3% on C3) */
-template <bool COUNT, int MEM, bool FMA = HRT_BOX_FMA && MEM != WM_HYB>
+template <bool COUNT, int MEM, bool FMA = HRT_BOX_FMA && (MEM != WM_HYB || HRT_BOX_FMA_ALL)>
 HRT_LANE_FI void walk_box(const WalkSrc& src, uint32_t& i, const TRay& r, float tmin, float closest, Counts& cn) {
   const float4 a = wload<MEM>(src, i), b = wload<MEM>(src, i + 16u);
   uint32_t skip = f2u(a.w);

@@ -97,6 +97,29 @@ def test_cornell_group_box_pixel(earth):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("tile", [(1568, 224), (400, 240), (1632, 1568)])
+def test_c5_share_tiles_at_10000spp(tile, earth):
+    """Three 16-px tiles of C5's 1/8 share (Cornell 2048^2, 10000 spp) rendered as the share's tiles: the
+    general kernel's earlier box form (sub/mul/add, before r03v) took a different path in one sample of each
+    (+-45 world.hit calls, the image unchanged: the paths miss the light); ray counts must equal the oracle's."""
+    import torch
+
+    x, y = tile
+    W = H = 2048
+    s = hrt.preset("cornell", 1, earth)
+    s.commit()
+    cam = hrt.preset_camera(s.info, W, H)
+    p = hrt.params(W, H, 10000, 50, 1, tuple(s.info.background))
+    d = torch.empty(16 * 16 * 4, dtype=torch.float32, device="cuda")
+    st = hrt.render_tiles_device(s, cam, p, [(x, y, 16, 16)], d.data_ptr(), 0, want_stats=True)
+    img = d.view(16, 16, 4).cpu().numpy()
+    ref, cnt = O.OracleScene(hrt.PRESETS["cornell"], 1, earth).render(W, H, 10000, 50, seed=1, region=(x, y, 16, 16),
+                                                                      threads=THREADS)
+    assert st.segments == cnt["segments"], (st.segments, cnt["segments"])
+    assert np.abs(img - ref).max() <= TOL
+
+
+@pytest.mark.gpu
 def test_device_built_walk_vs_oracle(earth):
     """A scene of 39.9k leaves (random_40k: the Random builder over a 200 x 200 grid) takes the
     device-side build of the walk hierarchy by default (build_walk.hip, >= 32768 leaves); its frame band
