@@ -365,7 +365,9 @@ struct Plan {
 
 Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
   Plan pl;
-  pl.full = (s->feature_mask & ~G::F_BASIC) != 0;
+  /* a sphere scene whose walk stream is the GENERAL one (a List inside a BvhNode leaf: scene.cpp build_walk)
+   * runs the general kernels: the sphere kernel would read its 48-B leaf programs as sphere payloads */
+  pl.full = (s->feature_mask & ~G::F_BASIC) != 0 || s->w_general;
   pl.heavy = false;
   pl.perlin_lds = false;
   /* default: exact.  A ray time outside the interval the BVH boxes were built for can put a moving

@@ -268,6 +268,11 @@ namespace hrt {
 void launch_sphere(int cull, bool count, bool lds, bool heavy, const KParams& kp, int device, hipStream_t stream,
                    size_t smem) {
   if (heavy) { /* noise / image textures (exact culling only: plan()) */
+    if (lds && kp.walk_hot > 0) { /* a stream beyond the LDS budget: its staged part in LDS, the rest global */
+      count ? launch_basic<G::CULL_EXACT, true, true, true, true>(kp, device, stream, smem)
+            : launch_basic<G::CULL_EXACT, false, true, true, true>(kp, device, stream, smem);
+      return;
+    }
     if (count) lds ? launch_basic<G::CULL_EXACT, true, true, false, true>(kp, device, stream, smem)
                    : launch_basic<G::CULL_EXACT, true, false, false, true>(kp, device, stream, 0);
     else lds ? launch_basic<G::CULL_EXACT, false, true, false, true>(kp, device, stream, smem)

@@ -950,7 +950,8 @@ std::vector<WalkLeaf> walk_leaves(const hrt_scene* s, std::vector<WNode>* ref_tr
  * hierarchy node when its subtree holds a box node outside every instance bracket (its children are
  * BvhNodes); otherwise it is a leaf, its program the whole subtree (boxes inside instances included:
  * trace_ray walks them in the instance's frame). */
-std::vector<WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<WNode>* ref_tree, bool* regroup_ok) {
+std::vector<WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<WNode>* ref_tree, bool* regroup_ok,
+                                   const std::vector<char>* whole) {
   const uint32_t n = s->main_end;
   const float inf = u2f(0x7f800000u);
   std::vector<WalkLeaf> leaves;
@@ -1181,6 +1182,7 @@ std::vector<WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<WNode>* ref_t
         else if (k == G::K_INST_END) depth--;
         else if (depth == 0 && (k == G::K_BOX || k == G::K_BOX_PRIM)) hierarchy = true;
       }
+      if (hierarchy && whole && (*whole)[i]) hierarchy = false; /* kept whole (gwalk_leaves_grouped) */
       if (hierarchy) {
         T.push_back(WNode{node_box(i), -1, skip, (uint32_t)open.size()});
         start.push_back(i);
@@ -1254,6 +1256,35 @@ std::vector<WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<WNode>* ref_t
   return leaves;
 }
 
+/* The group-box state of a lane (lane.h gwalk_leaf_test gstate) remembers the outcome of the LAST group
+ * whose box it tested.  A group's box-less leaves must therefore be contiguous in the leaf sequence: a
+ * List inside a BvhNode leaf whose members come before AND after a nested BvhNode holding box-less members
+ * of its own would re-test the outer box with a smaller closest after the inner group (the reference tests
+ * it once, G19).  Such a box is kept as one leaf whose program is its whole subtree (trace_ray walks it
+ * in the reference's order), which the leaf sequence is rebuilt with. */
+std::vector<WalkLeaf> gwalk_leaves_grouped(const hrt_scene* s, std::vector<WNode>* ref_tree, bool* regroup_ok) {
+  const char* ge = getenv("HRT_GWALK_GROUPED"); /* "0": no fallback (tests show the case it covers) */
+  if (ge && strcmp(ge, "0") == 0) return gwalk_leaves(s, ref_tree, regroup_ok);
+  std::vector<char> whole(s->g_nodes.size(), 0);
+  for (;;) {
+    std::vector<WalkLeaf> leaves = gwalk_leaves(s, ref_tree, regroup_ok, &whole);
+    std::vector<char> closed(s->g_nodes.size(), 0);
+    uint32_t cur = G::NONE;
+    bool again = false;
+    for (const WalkLeaf& L : leaves) {
+      if (!L.has_rbox || L.rgroup == cur) continue;
+      if (cur != G::NONE) closed[cur] = 1;
+      cur = L.rgroup;
+      if (closed[cur]) { /* the group comes back after another one: keep its box whole */
+        need(!whole[cur], HRT_ERR_STATE, "general walk stream: group kept whole twice");
+        whole[cur] = 1;
+        again = true;
+      }
+    }
+    if (!again) return leaves;
+  }
+}
+
 void build_walk(hrt_scene* s) {
   s->w_stream.clear();
   s->w_end = 0;
@@ -1267,7 +1298,7 @@ void build_walk(hrt_scene* s) {
     if ((gw && strcmp(gw, "0") == 0) || s->media_nested) return;
     std::vector<WNode> T;
     bool regroup_ok = false;
-    const std::vector<WalkLeaf> leaves = gwalk_leaves(s, &T, &regroup_ok);
+    const std::vector<WalkLeaf> leaves = gwalk_leaves_grouped(s, &T, &regroup_ok);
     if (leaves.empty()) return;
     s->w_general = true;
     const char* mode = getenv("HRT_WALK_TREE");
@@ -1290,7 +1321,7 @@ void build_walk(hrt_scene* s) {
                        * which the general stream's group test does (render_gwalk_kernel) */
       std::vector<WNode> TG;
       bool gok = false;
-      const std::vector<WalkLeaf> gl = gwalk_leaves(s, &TG, &gok);
+      const std::vector<WalkLeaf> gl = gwalk_leaves_grouped(s, &TG, &gok);
       s->w_general = true;
       const char* md = getenv("HRT_WALK_TREE");
       if (gok && !(md && strcmp(md, "reference") == 0)) {

@@ -171,8 +171,12 @@ std::vector<uint8_t> build_blob(hrt_scene* s); /* scene.cpp: the arrays in one b
  * and the placement + records of a hierarchy over them */
 std::vector<host::WalkLeaf> walk_leaves(const hrt_scene* s, std::vector<host::WNode>* ref_tree, bool* regroup_ok);
 void walk_place_and_write(hrt_scene* s, const std::vector<host::WNode>& T, const std::vector<host::WalkLeaf>& leaves);
-/* scene.cpp: the general-scene walk stream's leaf objects (layout.h) in the reference's pre-order */
-std::vector<host::WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<host::WNode>* ref_tree, bool* regroup_ok);
+/* scene.cpp: the general-scene walk stream's leaf objects (layout.h) in the reference's pre-order; a
+ * BvhNode box whose reference-stream index is marked in `whole` stays ONE leaf (its subtree the program),
+ * and gwalk_leaves_grouped marks every box whose group's box-less leaves would not be contiguous */
+std::vector<host::WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<host::WNode>* ref_tree, bool* regroup_ok,
+                                         const std::vector<char>* whole = nullptr);
+std::vector<host::WalkLeaf> gwalk_leaves_grouped(const hrt_scene* s, std::vector<host::WNode>* ref_tree, bool* regroup_ok);
 /* build_walk.hip: the re-grouped hierarchy (scene.cpp walk_regroup's splits) built on the device */
 void device_walk_regroup(const std::vector<host::WalkLeaf>& leaves, std::vector<host::WNode>& T, int device);
 void device_release(hrt_scene* s);

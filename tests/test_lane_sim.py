@@ -313,3 +313,36 @@ def test_exact_culling_property_on_grazing_rays(sim):
     print("cull property totals", total)
     assert accepted > 100000 and outside > 0  # grazing false hits were produced and none was culled
     assert raised >= 60 and nan_rays > 0
+
+
+def sim_render_scene(L, s, w, h, spp, kernel, cull, seed=11):
+    """sim_render for a scene built through the ABI's constructors (tests/scenes.py)."""
+    import scenes
+
+    blob, info = hrt.scene_blob(s)
+    cam = scenes.camera(w, h)
+    p = hrt.params(w, h, spp, 50, seed)
+    out = np.zeros((h, w, 4), np.float32)
+    cnt = np.zeros(8, np.uint64)
+    rc = L.lane_sim_render(blob, ctypes.byref(info), ctypes.byref(cam), ctypes.byref(p), kernel, cull, 0, 0, w, h,
+                           out.ctypes.data_as(ctypes.c_void_p), cnt.ctypes.data_as(ctypes.c_void_p))
+    return rc, out, {"segments": int(cnt[0]), "nodes": int(cnt[2]), "prims": int(cnt[3])}
+
+
+def test_custom_scenes_exact_lanes_equal_reference_traversal(sim):
+    """sphere-only scenes with Lists in BvhNodes walk the GENERAL stream (render_gwalk_kernel's
+    lane; the sphere lane refuses it), a List around a nested BvhNode of Lists keeps its group whole, and a
+    textured sphere scene beyond the LDS budget walks the sphere stream (HEAVY): each bit for bit equal to
+    the verbatim reference traversal of the segment kernel's lane."""
+    import scenes
+
+    for make, kernel, (w, h, spp) in ((scenes.sphere_lists, 3, (48, 27, 6)), (scenes.big_textured, 0, (48, 27, 4))):
+        s = make()
+        rc, a, sa = sim_render_scene(sim, s, w, h, spp, kernel, CULL_EXACT)
+        assert rc == 0
+        rc, b, sb = sim_render_scene(sim, s, w, h, spp, 2, CULL_REFERENCE)
+        assert rc == 0
+        assert sa["segments"] == sb["segments"] and np.array_equal(a, b), make.__name__
+        assert sa["nodes"] < sb["nodes"]
+    rc, _, _ = sim_render_scene(sim, scenes.sphere_lists(), 8, 8, 1, 0, CULL_EXACT)
+    assert rc == 1  # no sphere stream: the sphere kernel's lane must not run it
