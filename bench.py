@@ -79,6 +79,8 @@ def parse():
                     help="every rank on GPU 0 (rehearsal of the N > 1 path on a one-GPU box; not a scaling figure)")
     ap.add_argument("--share", type=int, default=1,
                     help="one process: render rank 0's share of an N-way tile split (one GPU's part of an N-GPU frame)")
+    ap.add_argument("--launch-record", default="",
+                    help="write the timed launch's record (hrt_last_launch: kernel, grid, occupancy, VGPRs, scratch) here")
     ap.add_argument("--no-delivery", action="store_true",
                     help="skip the per-frame delivery phase (frame_ms: launch + D2H + host placement, pipelined)")
     return ap.parse_args()
@@ -203,7 +205,9 @@ def apply_pmc(ro, key, pm, launch_s, seg_step):
     """Fill the roofline object's counter fields from the PMC record of this launch's workload (`key`);
     counters that would put the launch above peak belong to another workload and are rejected."""
     ro["pmc_key"] = key
-    if pm and pm.get("valu_insts"):
+    if pm and pm.get("rejected"):
+        ro["pmc_rejected"] = pm["rejected"]
+    elif pm and pm.get("valu_insts"):
         sha = hashlib.sha256(open(hrt.LIB_PATH, "rb").read()).hexdigest()[:16]
         ach = pm["valu_insts"] / launch_s / 1e9
         ro.update(achieved=round(ach, 1), frac=round(ach / ro["peak"], 4), traffic=pm.get("hbm_bytes"),
@@ -382,6 +386,11 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     scene.synchronize()  # raises if the walk watchdog stopped any timed launch (incomplete frame)
+    launch = hrt.last_launch()  # what the timed steps ran: kernel, persistent grid, occupancy, VGPRs, scratch
+    if args.launch_record:
+        os.makedirs(os.path.dirname(os.path.abspath(args.launch_record)), exist_ok=True)
+        with open(args.launch_record, "w") as fh:
+            json.dump(launch, fh)
     log(f"timed steps done: {dt / args.steps * 1e3:.1f} ms per step", all_ranks=True)
     launch_ms = sum(a.elapsed_time(b) for a, b in ev) / max(1, args.steps)
     rank_ms = [round(launch_ms, 2)]
@@ -483,6 +492,7 @@ def main():
                     "share_pixels": n_px} if world == 1 and share > 1 else {}),
                 "cull_mode": {0: "reference", 1: "slab (approximate)", 2: "exact (reference test + provably safe culling)"}[si.cull_mode],
             },
+            "launch": launch,
             "parity": parity,
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -22,7 +22,9 @@ struct HipError {
 };
 void hip_check(hipError_t e, const char* what);
 /* persistent grid: as many workgroups as are co-resident on the device (cached per kernel/device) */
-int resident_grid(const void* fn, int block, int device, size_t smem, bool lds);
+/* the persistent grid of a kernel (occupancy x CUs, cached); records the launch for hrt_last_launch
+ * (`name`: the launcher's __PRETTY_FUNCTION__, whose template arguments name the instantiation) */
+int resident_grid(const void* fn, int block, int device, size_t smem, bool lds, const char* name);
 /* render_sphere.hip: launch render_basic_kernel<cull, count, lds> */
 void launch_sphere(int cull, bool count, bool lds, bool heavy, const lane::KParams& kp, int device, hipStream_t stream,
                    size_t smem);

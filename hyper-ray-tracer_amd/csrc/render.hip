@@ -267,6 +267,25 @@ __global__ void math_kernel(int op, const float* x, const float* y, float* out, 
   out[i] = r;
 }
 
+/* hrt_debug_box_test: the walk's inflated box test (lane.h box_ce) on (box, ray) pairs, the same code on the
+ * device and on the host (this file's host compilation of lane.h) */
+template <bool FMA>
+HRT_LANE_FI uint8_t box_pair(const float* boxes, const float* rays, uint32_t b, uint32_t q, float tmin, float tmax) {
+  TRay r;
+  set_dir(r, v3(rays[6 * q], rays[6 * q + 1], rays[6 * q + 2]), v3(rays[6 * q + 3], rays[6 * q + 4], rays[6 * q + 5]));
+  const float4 c = make_float4(boxes[8 * b], boxes[8 * b + 1], boxes[8 * b + 2], 0.0f);
+  const float4 e = make_float4(boxes[8 * b + 4], boxes[8 * b + 5], boxes[8 * b + 6], 0.0f);
+  return box_ce<FMA>(c, e, r, tmin, tmax) ? 1u : 0u;
+}
+
+__global__ void box_test_kernel(int form, const float* boxes, uint32_t nb, const float* rays, uint32_t nr, float tmin,
+                                float tmax, uint8_t* out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (uint64_t)nb * nr) return;
+  const uint32_t b = (uint32_t)(i / nr), q = (uint32_t)(i % nr);
+  out[i] = form ? box_pair<true>(boxes, rays, b, q, tmin, tmax) : box_pair<false>(boxes, rays, b, q, tmin, tmax);
+}
+
 /* ------------------------------------------------------------------ host helpers */
 struct DeviceGuard {
   int prev = -1;
@@ -327,7 +346,7 @@ template <int CULL, bool FULL, bool COUNT, bool LDS, bool FAST, int GW = 0, int 
 void launch(const KParams& kp, int device, hipStream_t stream, size_t smem) {
   const void* fn = (const void*)render_kernel<CULL, FULL, COUNT, LDS, FAST, GW, TRIM>;
   const int block = general_block_threads<FULL, LDS, FAST>();
-  const int grid = resident_grid(fn, block, device, LDS ? smem : 0, LDS);
+  const int grid = resident_grid(fn, block, device, LDS ? smem : 0, LDS, __PRETTY_FUNCTION__);
   hipLaunchKernelGGL((render_kernel<CULL, FULL, COUNT, LDS, FAST, GW, TRIM>), dim3(grid), dim3(block), LDS ? smem : 0,
                      stream, kp);
   hip_check(hipGetLastError(), "render_kernel launch");
@@ -337,7 +356,7 @@ template <int CULL, bool COUNT, bool LDS>
 void launch_full(const KParams& kp, int device, hipStream_t stream, size_t smem) {
   const void* fn = (const void*)render_full_kernel<CULL, COUNT, LDS>;
   const int block = basic_block_threads<LDS, FULL_WAVES>();
-  const int grid = resident_grid(fn, block, device, LDS ? smem : 0, LDS);
+  const int grid = resident_grid(fn, block, device, LDS ? smem : 0, LDS, __PRETTY_FUNCTION__);
   hipLaunchKernelGGL((render_full_kernel<CULL, COUNT, LDS>), dim3(grid), dim3(block), LDS ? smem : 0, stream, kp);
   hip_check(hipGetLastError(), "render_full_kernel launch");
 }
@@ -621,18 +640,39 @@ void hip_check(hipError_t e, const char* what) {
   if (e != hipSuccess) throw HipError{HRT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e)};
 }
 
-int resident_grid(const void* fn, int block, int device, size_t smem, bool lds) {
-  struct Key {
-    const void* fn;
-    int device;
-    size_t smem;
-    int grid;
-  };
+namespace {
+struct GridKey {
+  const void* fn;
+  int device;
+  size_t smem;
+  hrt_launch_info info;
+};
+thread_local hrt_launch_info t_last_launch;
+thread_local bool t_has_launch = false;
+
+/* "void ns::launch_basic(...) [CULL = 2, COUNT = false, ...]" -> "launch_basic[CULL = 2, COUNT = false, ...]" */
+void launch_name(const char* pretty, char* out, size_t cap) {
+  std::string s(pretty ? pretty : "?");
+  const size_t paren = s.find('(');
+  std::string head = s.substr(0, paren);
+  const size_t sp = head.find_last_of(" :");
+  head = sp == std::string::npos ? head : head.substr(sp + 1);
+  const size_t br = s.find('[');
+  std::string name = head + (br == std::string::npos ? std::string() : s.substr(br));
+  snprintf(out, cap, "%s", name.c_str());
+}
+}  // namespace
+
+int resident_grid(const void* fn, int block, int device, size_t smem, bool lds, const char* name) {
   static std::mutex mu;
-  static std::vector<Key> cache;
+  static std::vector<GridKey> cache;
   std::lock_guard<std::mutex> lk(mu);
-  for (const Key& k : cache)
-    if (k.fn == fn && k.device == device && k.smem == smem) return k.grid;
+  for (const GridKey& k : cache)
+    if (k.fn == fn && k.device == device && k.smem == smem) {
+      t_last_launch = k.info;
+      t_has_launch = true;
+      return (int)k.info.grid;
+    }
   if (lds) hip_check(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem),
                      "hipFuncSetAttribute(LDS)");
   int per_cu = 0;
@@ -640,8 +680,24 @@ int resident_grid(const void* fn, int block, int device, size_t smem, bool lds) 
             "hipOccupancyMaxActiveBlocksPerMultiprocessor");
   hipDeviceProp_t prop;
   hip_check(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
+  hipFuncAttributes fa;
+  memset(&fa, 0, sizeof(fa));
+  hip_check(hipFuncGetAttributes(&fa, fn), "hipFuncGetAttributes");
   const int g = std::max(1, per_cu) * prop.multiProcessorCount;
-  cache.push_back(Key{fn, device, smem, g});
+  hrt_launch_info li;
+  memset(&li, 0, sizeof(li));
+  launch_name(name, li.kernel, sizeof(li.kernel));
+  li.grid = (uint32_t)g;
+  li.block = (uint32_t)block;
+  li.blocks_per_cu = (uint32_t)std::max(0, per_cu);
+  li.cus = (uint32_t)prop.multiProcessorCount;
+  li.waves_per_simd = li.blocks_per_cu * (uint32_t)block / 64u / 4u;
+  li.vgprs = (uint32_t)fa.numRegs;
+  li.scratch_bytes = (uint32_t)fa.localSizeBytes;
+  li.lds_bytes = (uint32_t)smem;
+  cache.push_back(GridKey{fn, device, smem, li});
+  t_last_launch = li;
+  t_has_launch = true;
   return g;
 }
 
@@ -1058,6 +1114,45 @@ hrt_status hrt_debug_trace_path(hrt_scene* s, const hrt_camera* cam, const hrt_r
     hip_check(hipMemcpy(n_segments, d_n, 4, hipMemcpyDeviceToHost), "hipMemcpy");
     (void)hipFree(d_out);
     (void)hipFree(d_n);
+  });
+}
+
+hrt_status hrt_debug_box_test(int32_t form, int32_t on_device, const float* boxes, uint32_t n_boxes, const float* rays,
+                              uint32_t n_rays, float tmin, float tmax, uint8_t* out) {
+  return hguard([&] {
+    if (!boxes || !rays || !out || form < 0 || form > 1 || (uint64_t)n_boxes * n_rays >= (1ull << 31))
+      throw HipError{HRT_ERR_INVALID_ARG, "hrt_debug_box_test: bad argument"};
+    const uint64_t n = (uint64_t)n_boxes * n_rays;
+    if (n == 0) return;
+    if (!on_device) {
+      for (uint32_t b = 0; b < n_boxes; b++)
+        for (uint32_t q = 0; q < n_rays; q++)
+          out[(uint64_t)b * n_rays + q] = form ? box_pair<true>(boxes, rays, b, q, tmin, tmax)
+                                               : box_pair<false>(boxes, rays, b, q, tmin, tmax);
+      return;
+    }
+    float *db = nullptr, *dr = nullptr;
+    uint8_t* dout = nullptr;
+    hip_check(hipMalloc((void**)&db, (size_t)n_boxes * 32), "hipMalloc");
+    hip_check(hipMalloc((void**)&dr, (size_t)n_rays * 24), "hipMalloc");
+    hip_check(hipMalloc((void**)&dout, n), "hipMalloc");
+    hip_check(hipMemcpy(db, boxes, (size_t)n_boxes * 32, hipMemcpyHostToDevice), "hipMemcpy");
+    hip_check(hipMemcpy(dr, rays, (size_t)n_rays * 24, hipMemcpyHostToDevice), "hipMemcpy");
+    hipLaunchKernelGGL(box_test_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, form, db, n_boxes, dr, n_rays,
+                       tmin, tmax, dout);
+    hip_check(hipGetLastError(), "box_test_kernel launch");
+    hip_check(hipMemcpy(out, dout, n, hipMemcpyDeviceToHost), "hipMemcpy");
+    (void)hipFree(db);
+    (void)hipFree(dr);
+    (void)hipFree(dout);
+  });
+}
+
+hrt_status hrt_last_launch(hrt_launch_info* out) {
+  return hguard([&] {
+    if (!out) throw HipError{HRT_ERR_INVALID_ARG, "hrt_last_launch: null pointer"};
+    if (!t_has_launch) throw HipError{HRT_ERR_STATE, "hrt_last_launch: no launch on this thread yet"};
+    *out = t_last_launch;
   });
 }
 

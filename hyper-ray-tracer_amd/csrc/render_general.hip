@@ -245,7 +245,7 @@ void launch_g(const KParams& kp, int device, hipStream_t stream, size_t smem) {
   KParams p = kp;
   p.lane_lds = (uint32_t)((smem + 15) & ~(size_t)15);
   const size_t total = p.lane_lds + (size_t)block * sizeof(uint32_t);
-  const int grid = resident_grid(fn, block, device, total, true);
+  const int grid = resident_grid(fn, block, device, total, true, __PRETTY_FUNCTION__);
   hipLaunchKernelGGL((render_gwalk_kernel<COUNT, WMEM, LREF, TRIM>), dim3(grid), dim3(block), total, stream, p);
   hip_check(hipGetLastError(), "render_gwalk_kernel launch");
 }

@@ -255,7 +255,7 @@ void launch_basic(const KParams& kp, int device, hipStream_t stream, size_t smem
   KParams p = kp;
   p.lane_lds = LDS ? (uint32_t)((smem + 15) & ~(size_t)15) : 0u;
   const size_t total = p.lane_lds + (size_t)block * sizeof(uint32_t);
-  const int grid = resident_grid(fn, block, device, total, true);
+  const int grid = resident_grid(fn, block, device, total, true, __PRETTY_FUNCTION__);
   hipLaunchKernelGGL((render_basic_kernel<CULL, COUNT, LDS, HYB, HEAVY>), dim3(grid), dim3(block), total, stream, p);
   hip_check(hipGetLastError(), "render_basic_kernel launch");
 }

@@ -132,6 +132,14 @@ class SceneInfo(ctypes.Structure):
     ]
 
 
+class LaunchInfo(ctypes.Structure):
+    """hrt_launch_info: the last render launch of the calling thread (hrt_last_launch)."""
+    _fields_ = [("kernel", ctypes.c_char * 160)] + [
+        (n, ctypes.c_uint32) for n in ("grid", "block", "blocks_per_cu", "cus", "waves_per_simd", "vgprs", "scratch_bytes",
+                                       "lds_bytes")
+    ]
+
+
 # Every entry point of include/hrt/hrt.h (tests/test_abi.py checks the header against this list).
 EXPORTS = [
     "hrt_last_error", "hrt_version", "hrt_scene_create", "hrt_scene_destroy",
@@ -140,7 +148,7 @@ EXPORTS = [
     "hrt_node_sphere", "hrt_node_moving_sphere", "hrt_node_rect", "hrt_node_cuboid", "hrt_node_translate",
     "hrt_node_rotate", "hrt_node_constant_medium", "hrt_node_list", "hrt_node_bvh", "hrt_node_count",
     "hrt_node_bounding_box", "hrt_scene_set_root", "hrt_scene_commit", "hrt_preset_build", "hrt_camera_init",
-    "hrt_render_tiles_device", "hrt_render_device", "hrt_render", "hrt_tile_grid", "hrt_scene_get_info",
+    "hrt_render_tiles_device", "hrt_render_device", "hrt_render", "hrt_tile_grid", "hrt_scene_get_info", "hrt_last_launch", "hrt_debug_box_test",
     "hrt_debug_device_math", "hrt_debug_trace_path", "hrt_debug_scene_blob", "hrt_image_write", "hrt_render_progressive", "hrt_debug_prim_record",
     "hrt_scene_synchronize", "hrt_debug_poke_blob",
 ]
@@ -203,6 +211,9 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hrt_render": (S, [vp, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), u32, u32, u32, u32, vp, ctypes.POINTER(RenderStats)]),
         "hrt_tile_grid": (S, [u32, u32, u32, u32, u32, vp, u32, _U32P]),
         "hrt_scene_get_info": (S, [vp, ctypes.POINTER(SceneInfo)]),
+        "hrt_last_launch": (S, [ctypes.POINTER(LaunchInfo)]),
+        "hrt_debug_box_test": (S, [ctypes.c_int32, ctypes.c_int32, vp, ctypes.c_uint32, vp, ctypes.c_uint32, ctypes.c_float,
+                                   ctypes.c_float, vp]),
         "hrt_debug_device_math": (S, [i32, vp, vp, vp, u32]),
         "hrt_debug_scene_blob": (S, [vp, vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(BlobInfo)]),
         "hrt_debug_prim_record": (S, [vp, i32, u32, vp]),
@@ -450,6 +461,26 @@ def render_tiles_device(scene: Scene, cam: Camera, p: RenderParams, tiles, d_out
     _check(load().hrt_render_tiles_device(scene.h, ctypes.byref(cam), ctypes.byref(p), ctypes.cast(arr, ctypes.c_void_p), len(tiles),
                                           ctypes.c_void_p(d_out_ptr), ctypes.c_void_p(stream_ptr), ctypes.byref(st) if want_stats else None))
     return st if want_stats else None
+
+
+def last_launch() -> dict:
+    """The calling thread's last render launch (hrt_last_launch): kernel, grid, occupancy, VGPRs, scratch, LDS."""
+    li = LaunchInfo()
+    _check(load().hrt_last_launch(ctypes.byref(li)))
+    d = {n: getattr(li, n) for n, _ in LaunchInfo._fields_[1:]}
+    d["kernel"] = li.kernel.decode()
+    d["waves"] = li.grid * li.block // 64
+    return d
+
+
+def box_test(form: int, boxes: np.ndarray, rays: np.ndarray, tmin: float, tmax: float, on_device: bool = True) -> np.ndarray:
+    """hrt_debug_box_test: (n_boxes, n_rays) uint8 pass flags of the walk's inflated box test (form 0 / 1)."""
+    b = np.ascontiguousarray(boxes, np.float32).reshape(-1, 8)
+    r = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
+    out = np.zeros((len(b), len(r)), np.uint8)
+    _check(load().hrt_debug_box_test(form, 1 if on_device else 0, b.ctypes.data, len(b), r.ctypes.data, len(r), tmin, tmax,
+                                     out.ctypes.data))
+    return out
 
 
 def device_math(op: int, x: np.ndarray, y: Optional[np.ndarray] = None) -> np.ndarray:

@@ -280,6 +280,21 @@ typedef struct hrt_scene_info {
   uint32_t walk_build_us;  /* the re-grouping's time, host or device (us) */
 } hrt_scene_info;
 hrt_status hrt_scene_get_info(const hrt_scene* s, hrt_scene_info* info);
+/* The last render launch the calling thread made (thread-local, like hrt_last_error): the kernel, its
+ * persistent grid and the occupancy answer it was sized by (hipOccupancyMaxActiveBlocksPerMultiprocessor),
+ * and the kernel's registers, scratch and LDS (hipFuncGetAttributes), so that a measurement records what
+ * ran.  HRT_ERR_STATE before the thread's first launch. */
+typedef struct hrt_launch_info {
+  char kernel[160];        /* the kernel and its template arguments */
+  uint32_t grid, block;    /* workgroups launched, threads per workgroup */
+  uint32_t blocks_per_cu;  /* resident workgroups per CU (the occupancy answer) */
+  uint32_t cus;            /* compute units of the device */
+  uint32_t waves_per_simd; /* blocks_per_cu * block / 64 / 4 */
+  uint32_t vgprs;          /* registers per lane */
+  uint32_t scratch_bytes;  /* private (scratch) bytes per lane: register spills and stack */
+  uint32_t lds_bytes;      /* dynamic LDS per workgroup */
+} hrt_launch_info;
+hrt_status hrt_last_launch(hrt_launch_info* out);
 /* Write an RGBA f32 frame (w x h, row-major, row 0 = image y 0 = bottom, as the render calls produce;
  * alpha is dropped) to `path` in an HRT_IMAGE_* format. */
 hrt_status hrt_image_write(const char* path, const float* rgba, uint32_t w, uint32_t h, int32_t format);
@@ -325,6 +340,13 @@ hrt_status hrt_debug_prim_record(const hrt_scene* s, int32_t order, uint32_t ind
  * 5 pow5, 6 tan, 7 the walk's division x / y) for n inputs; used by the GPU KAT test to prove
  * host/device bit identity. */
 hrt_status hrt_debug_device_math(int32_t op, const float* x, const float* y, float* out, uint32_t n);
+/* The walk's inflated box test (CULL_EXACT's culling half, lane.h box_ce; form 0: sub/mul/add, 1: the fused
+ * o*inv form) on every (box, ray) pair, on the DEVICE (on_device = 1) or with the same code compiled for
+ * the host (0): boxes n_boxes x 8 floats (C.xyz, -, E.xyz, -), rays n_rays x 6 floats (origin, direction),
+ * out[b * n_rays + q] = 1 if box b passes for ray q on [tmin, tmax].  Used by the GPU test that holds the
+ * device's culling decisions to the host's bit for bit. */
+hrt_status hrt_debug_box_test(int32_t form, int32_t on_device, const float* boxes, uint32_t n_boxes, const float* rays,
+                              uint32_t n_rays, float tmin, float tmax, uint8_t* out);
 
 #ifdef __cplusplus
 }

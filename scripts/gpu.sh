@@ -52,6 +52,7 @@ profile() {  # profile <tag> <preset> <W> <H> <spp> [share] [bench args...]
     local pass=$1; shift
     echo "== profile $tag $pass" >> "$LOG"
     timeout -k 10 400 rocprofv3 "$@" -d "$OUT/prof_${tag}_$pass" -o run --output-format csv -- python3 "$ROOT/bench.py" $args \
+      --launch-record "$OUT/prof_${tag}_$pass/launch.json" \
       >> "$OUT/profile_$tag.log" 2>&1
     local r=$?
     echo "== profile $tag $pass exit $r" >> "$LOG"

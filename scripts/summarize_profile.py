@@ -8,8 +8,12 @@ bench.py reads for its `roofline` object:
   - clock_hz    : GRBM_GUI_ACTIVE / 8 XCDs / kernel time (MI355X_MICROARCH.md, DVFS give-back);
   - hbm_bytes   : 2 x FETCH_SIZE + WRITE_SIZE (FETCH_SIZE doubled per the gfx950 note of the guide);
   - lds_*       : SQ_INSTS_LDS, SQ_LDS_BANK_CONFLICT, SQ_LDS_IDX_ACTIVE;
-  - lib_sha16   : which libhrt.so build the counters belong to (bench reports whether it matches).
+  - lib_sha16   : which libhrt.so build the counters belong to (bench reports whether it matches);
+  - launch      : bench.py's record of the launch (hrt_last_launch: kernel, grid, occupancy, VGPRs, scratch).
 The launch profiled is the first timed-kernel dispatch of the run (the warm-up frame with stats).
+A record whose SQ_WAVES differs from the waves the launch record says were launched (grid x block / 64) is
+REJECTED: its counters describe another launch shape (a box whose occupancy answer differed, another
+build), so bench.py does not price a launch with them.
 """
 import csv
 import hashlib
@@ -121,6 +125,25 @@ def main():
                 wc = c["SQ_WAVE_CYCLES"]
                 lines.append(f"\n**Wave time**: issuing {c['SQ_ACTIVE_INST_ANY']/wc*100:.1f}%, waiting to issue (pipe busy / "
                              f"dependency) {c['SQ_WAIT_INST_ANY']/wc*100:.1f}%, waiting on s_waitcnt {c['SQ_WAIT_ANY']/wc*100:.1f}%")
+    launch = None
+    for name in ("sq2", "sq", "kt"):
+        lp = os.path.join(src, f"prof_{tag}_{name}", "launch.json")
+        if os.path.exists(lp):
+            launch = json.load(open(lp))
+            break
+    if launch:
+        res["launch"] = launch
+        lines.append(f"\n**Launch** (hrt_last_launch): `{launch['kernel'][:120]}`, grid {launch['grid']} x {launch['block']} "
+                     f"({launch['blocks_per_cu']} workgroups per CU x {launch['cus']} CUs, {launch['waves_per_simd']} waves/SIMD), "
+                     f"{launch['vgprs']} VGPRs, {launch['scratch_bytes']} B scratch per lane, {launch['lds_bytes']} B LDS")
+        want = launch["grid"] * launch["block"] // 64
+        if "SQ_WAVES" in c and int(round(c["SQ_WAVES"])) != want:
+            res["rejected"] = (f"SQ_WAVES {c['SQ_WAVES']:.0f} != the launch's {want} waves: the counters describe another "
+                               "launch shape")
+            lines.append(f"\n**REJECTED**: {res['rejected']}")
+    elif "--allow-no-launch" not in sys.argv:
+        res["rejected"] = "no launch record (bench.py --launch-record): the launch shape cannot be checked"
+        lines.append(f"\n**REJECTED**: {res['rejected']}")
     with open(os.path.join(dst, f"{tag}_summary.md"), "w") as fh:
         fh.write("\n".join(lines) + "\n")
     pj = os.path.join(dst, "roofline_pmc.json")

@@ -245,3 +245,55 @@ def test_trimmed_general_kernel_equals_all_feature_kernel(name, w, h, spp, earth
     b, sb = hrt.render(s, cam, p, stats=True)
     assert sa.segments == sb.segments
     assert np.array_equal(a, b)
+
+
+def _share_exact_vs_reference(name, W, H, spp, share, earth):
+    """rank 0's share (or the whole frame, share 1) on the default EXACT path and on the verbatim reference
+    traversal (HRT_RENDER_REFERENCE_CULL: aabb.rs's per-axis test alone, the segment kernel over the
+    reference node stream): np.array_equal and equal world.hit counts."""
+    import torch
+
+    from hrt import tiling
+
+    s = hrt.preset(name, 1, earth)
+    s.commit()
+    cam = hrt.preset_camera(s.info, W, H)
+    bg = tuple(s.info.background)
+    tiles = [(0, 0, W, H)] if share == 1 else tiling.split_tiles(W, H, share, 0)
+    n = tiling.share_pixels(tiles)
+    out = []
+    for flags in (0, hrt.RENDER_REFERENCE_CULL):
+        d = torch.empty(n * 4, dtype=torch.float32, device="cuda")
+        st = hrt.render_tiles_device(s, cam, hrt.params(W, H, spp, 50, 1, bg, flags=flags), tiles, d.data_ptr(), 0,
+                                     want_stats=True)
+        out.append((d.cpu().numpy(), int(st.segments), hrt.last_launch()["kernel"]))
+    (a, ra, ka), (b, rb, kb) = out
+    print(f"{name} {W}x{H} {spp} spp share 1/{share}: rays {ra} vs {rb}; {ka} vs {kb}")
+    assert ra == rb
+    assert np.array_equal(a, b)
+    assert np.isfinite(a).all()
+    return ka
+
+
+@pytest.mark.gpu
+def test_c3_full_frame_exact_equals_reference_traversal(earth):
+    """BASELINE config 3 (Earth + Perlin ground, 1920x1080, 1000 spp), the whole frame: the sphere kernel's
+    HEAVY walk bit for bit equal to the reference traversal."""
+    k = _share_exact_vs_reference("earth_perlin", 1920, 1080, 1000, 1, earth)
+    assert "HEAVY = true" in k
+
+
+@pytest.mark.gpu
+def test_c4_share8_exact_equals_reference_traversal(earth):
+    """BASELINE config 4 (10k spheres, 3840x2160, 2000 spp), one GPU's 1/8 share of the 8-GPU frame: the
+    hybrid LDS / global walk bit for bit equal to the reference traversal."""
+    k = _share_exact_vs_reference("random_10k", 3840, 2160, 2000, 8, earth)
+    assert "HYB = true" in k
+
+
+@pytest.mark.gpu
+def test_c5_share8_exact_equals_reference_traversal(earth):
+    """BASELINE config 5 (Cornell 2048^2, 10000 spp), one GPU's 1/8 share: the general walk kernel bit for bit
+    equal to the reference traversal (the share where r03's earlier box form diverged in five paths)."""
+    k = _share_exact_vs_reference("cornell", 2048, 2048, 10000, 8, earth)
+    assert "launch_g" in k

@@ -113,7 +113,7 @@ def test_rust_extern_block_matches_header():
 
 
 RUST_CTYPES = {"u32": ctypes.c_uint32, "i32": ctypes.c_int32, "u64": ctypes.c_uint64, "f32": ctypes.c_float,
-               "u8": ctypes.c_uint8}
+               "u8": ctypes.c_uint8, "c_char": ctypes.c_char}
 
 
 def _ctype_of(rust):
@@ -144,7 +144,7 @@ def _c_layout(structs, tmp_path):
 
 PY_CLASSES = {"hrt_camera": "Camera", "hrt_render_params": "RenderParams", "hrt_tile": "Tile",
               "hrt_render_stats": "RenderStats", "hrt_tile_pixels": "TilePixels", "hrt_blob_info": "BlobInfo",
-              "hrt_preset_info": "PresetInfo", "hrt_scene_info": "SceneInfo"}
+              "hrt_preset_info": "PresetInfo", "hrt_scene_info": "SceneInfo", "hrt_launch_info": "LaunchInfo"}
 
 
 def test_struct_sizes_and_offsets_match_c(tmp_path):
