@@ -633,12 +633,19 @@ HRT_LANE_FI void set_face_normal(Rec& rec, Vec3 dir, Vec3 outward) {
 }
 
 /* sphere.rs:31-35 */
-/* out of line: two f64 transcendentals, needed only under an ImageTexture */
-HRT_LANE_NI void sphere_uv(Vec3 p, float& u, float& v) {
+/* out of line: two f64 transcendentals, needed only under an ImageTexture; (u, v) returned in registers */
+struct UV {
+  float u, v;
+};
+HRT_LANE_NI UV sphere_uv_v(Vec3 p) {
   float theta = acos_f(-p.y);
   float phi = atan2_f(-p.z, p.x) + PI_F;
-  u = phi / (2.0f * PI_F);
-  v = theta / PI_F;
+  return UV{phi / (2.0f * PI_F), theta / PI_F};
+}
+HRT_LANE_FI void sphere_uv(Vec3 p, float& u, float& v) {
+  const UV r = sphere_uv_v(p);
+  u = r.u;
+  v = r.v;
 }
 
 /* Record of the winning leaf in world space (hit_record.rs, sphere.rs:57-73, rect.rs:70-83,
@@ -733,8 +740,10 @@ HRT_LANE Rec make_record(const KParams& P, uint32_t winner, float t, Vec3 wo, Ve
   }
 }
 
-/* perlin_noise.rs:80-123 */
-HRT_LANE float perlin_noise(const G::Perlin* pn, Vec3 point) {
+/* perlin_noise.rs:80-123 over tables read through `pn`: a generic pointer, or (device, tables staged in LDS by
+ * the kernel) an LDS address-space pointer, so the 8 x 4 gathers per call are ds_read, not flat loads */
+template <class PN>
+HRT_LANE_FI float perlin_noise_t(PN pn, Vec3 point) {
   int32_t i = sat_f2i32(floorf(point.x));
   int32_t j = sat_f2i32(floorf(point.y));
   int32_t k = sat_f2i32(floorf(point.z));
@@ -751,12 +760,57 @@ HRT_LANE float perlin_noise(const G::Perlin* pn, Vec3 point) {
     uint32_t px = pn->perm[0][(uint32_t)((i + x) & 255)];
     uint32_t py = pn->perm[1][(uint32_t)((j + y) & 255)];
     uint32_t pz = pn->perm[2][(uint32_t)((k + z) & 255)];
-    float4 g = ld4(pn->ranvec[px ^ py ^ pz]);
+    const uint32_t g_i = px ^ py ^ pz;
+    const Vec3 g = v3(pn->ranvec[g_i][0], pn->ranvec[g_i][1], pn->ranvec[g_i][2]);
     Vec3 weight = v3(u - (float)x, v - (float)y, w - (float)z);
     acc += ((float)x * u + (float)(1 - x) * (1.0f - u)) * ((float)y * v + (float)(1 - y) * (1.0f - v)) *
-           ((float)z * w + (float)(1 - z) * (1.0f - w)) * dot(v3(g.x, g.y, g.z), weight);
+           ((float)z * w + (float)(1 - z) * (1.0f - w)) * dot(g, weight);
   }
   return acc;
+}
+HRT_LANE float perlin_noise(const G::Perlin* pn, Vec3 point) { return perlin_noise_t(pn, point); }
+
+/* noise_texture.rs:24-31 + turbulence perlin_noise.rs:66-78 (the scalar part of the texture value) */
+template <class PN>
+HRT_LANE_FI float noise_value_t(PN pn, float scale, Vec3 p) {
+  Vec3 q = scale * p;
+  float accumulator = 0.0f, weight = 1.0f;
+#pragma unroll 1
+  for (int o = 0; o < 7; o++) { /* rolled: keeps the code (and the callers' register demand) small */
+    accumulator += weight * perlin_noise_t(pn, q);
+    weight *= 0.5f;
+    q = q * 2.0f;
+  }
+  return 1.0f + sin_f((scale * p.z) + (10.0f * fabsf(accumulator)));
+}
+
+/* The noise texture's value with its tables at `pn`.  PLDS (device): the tables are in LDS (`pn` a generic
+ * pointer into the kernel's staged tables: its low 32 bits are the LDS address).  Out of line, with every
+ * input passed by value (no caller struct through memory). */
+template <bool PLDS>
+HRT_LANE_NI float noise_value(const G::Perlin* pn, float scale, Vec3 p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (PLDS) {
+    typedef __attribute__((address_space(3))) const G::Perlin lds_perlin;
+    return noise_value_t((const lds_perlin*)(size_t)(uint32_t)(size_t)pn, scale, p);
+  }
+#endif
+  return noise_value_t(pn, scale, p);
+}
+
+/* image_texture.rs:36-62 */
+HRT_LANE_FI Vec3 image_value(const uint8_t* images, uint32_t off, uint32_t w, uint32_t h, uint32_t comps, float u, float v) {
+  if (w == 0) return v3(1.0f, 0.0f, 1.0f);
+  float uu = u < 0.0f ? 0.0f : (u > 1.0f ? 1.0f : u);
+  float vc = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
+  float vv = 1.0f - vc;
+  uint32_t ii = sat_f2u32(uu * (float)w);
+  uint32_t jj = sat_f2u32(vv * (float)h);
+  if (ii >= w) ii = w - 1;
+  if (jj >= h) jj = h - 1;
+  const uint8_t* px = images + off + ((size_t)jj * w + ii) * comps;
+  const float cs = 1.0f / 255.0f;
+  return v3(cs * (float)px[0], cs * (float)px[1], cs * (float)px[2]);
 }
 
 /* sign of sin_f(v) for 1e-6 <= |v| <= 1e6: sin_f reduces v by pi/2 (hd_math reduce_pio2, same
@@ -792,11 +846,9 @@ HRT_LANE_FI bool checker_odd(float vx, float vy, float vz) {
 }
 
 /* textures/.rs value() */
-HRT_LANE Vec3 tex_heavy(const KParams& P, const G::Tex& T, float u, float v, Vec3 p);
-HRT_LANE_FI Vec3 tex_heavy_inl(const KParams& P, const G::Tex& T, float u, float v, Vec3 p);
 
-/* INL: noise / image textures inline (a kernel with the registers to spare: a call saves and restores
- * the caller's live registers through scratch) instead of the out-of-line tex_heavy */
+/* INL: the noise texture's turbulence inline (a kernel with the registers to spare: a call saves and
+ * restores the caller's live registers through scratch) instead of the out-of-line noise_value */
 template <bool FULL, bool COUNT, bool INL = false>
 HRT_LANE Vec3 tex_value(const KParams& P, uint32_t id, float u, float v, Vec3 p, Counts& cn) {
   for (int guard = 0; guard < 64; guard++) {
@@ -807,48 +859,25 @@ HRT_LANE Vec3 tex_value(const KParams& P, uint32_t id, float u, float v, Vec3 p,
       id = checker_odd(10.0f * p.x, 10.0f * p.y, 10.0f * p.z) ? T.i0 : T.i1;
       continue;
     }
-    if constexpr (FULL && INL) return tex_heavy_inl(P, T, u, v, p);
-    if constexpr (FULL) return tex_heavy(P, T, u, v, p);
-    break;
-  }
-  return v3(0.0f, 0.0f, 0.0f);
-}
-
-/* Noise and image textures (a solid/checker chain ends in tex_value): out of line, so their
- * registers do not count towards the kernels' walk loops. */
-HRT_LANE_NI Vec3 tex_heavy(const KParams& P, const G::Tex& T, float u, float v, Vec3 p) { return tex_heavy_inl(P, T, u, v, p); }
-
-HRT_LANE_FI Vec3 tex_heavy_inl(const KParams& P, const G::Tex& T, float u, float v, Vec3 p) {
-  {
-    {
-      if (T.kind == G::T_NOISE) { /* noise_texture.rs:24-31 + turbulence perlin_noise.rs:66-78 */
+    if constexpr (FULL) {
+      if (T.kind == G::T_NOISE) { /* noise_texture.rs:24-31: 0.5 (1 + sin(...)) per channel */
         const G::Perlin* pn = P.perlin + T.i0;
-        float scale = T.a[0];
-        Vec3 q = scale * p;
-        float accumulator = 0.0f, weight = 1.0f;
-#pragma unroll 1
-        for (int o = 0; o < 7; o++) { /* rolled: keeps the callee (and so its callers) small */
-          accumulator += weight * perlin_noise(pn, q);
-          weight *= 0.5f;
-          q = q * 2.0f;
+        float s;
+        if constexpr (INL) {
+#if defined(__HIP_DEVICE_COMPILE__)
+          typedef __attribute__((address_space(3))) const G::Perlin lds_perlin;
+          if (P.perlin_lds) s = noise_value_t((const lds_perlin*)(size_t)(uint32_t)(size_t)pn, T.a[0], p);
+          else
+#endif
+            s = noise_value_t(pn, T.a[0], p);
+        } else {
+          s = P.perlin_lds ? noise_value<true>(pn, T.a[0], p) : noise_value<false>(pn, T.a[0], p);
         }
-        float s = 1.0f + sin_f((scale * p.z) + (10.0f * fabsf(accumulator)));
         return (v3(1.0f, 1.0f, 1.0f) * 0.5f) * s;
       }
-      if (T.kind == G::T_IMAGE) { /* image_texture.rs:36-62 */
-        if (T.i1 == 0) return v3(1.0f, 0.0f, 1.0f);
-        float uu = u < 0.0f ? 0.0f : (u > 1.0f ? 1.0f : u);
-        float vc = v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v);
-        float vv = 1.0f - vc;
-        uint32_t ii = sat_f2u32(uu * (float)T.i1);
-        uint32_t jj = sat_f2u32(vv * (float)T.i2);
-        if (ii >= T.i1) ii = T.i1 - 1;
-        if (jj >= T.i2) jj = T.i2 - 1;
-        const uint8_t* px = P.images + T.i0 + ((size_t)jj * T.i1 + ii) * T.i3;
-        const float cs = 1.0f / 255.0f;
-        return v3(cs * (float)px[0], cs * (float)px[1], cs * (float)px[2]);
-      }
+      if (T.kind == G::T_IMAGE) return image_value(P.images, T.i0, T.i1, T.i2, T.i3, u, v);
     }
+    break;
   }
   return v3(0.0f, 0.0f, 0.0f);
 }
@@ -997,8 +1026,8 @@ HRT_LANE_FI bool shade(const KParams& P, PathState& ps, uint32_t winner, float c
 #define HRT_HEAVY_INLINE 0 /* 1: the HEAVY instantiation evaluates textures inline (r03i A/B on C3: 16491 vs 17085 Mrays/s out of line) */
 #endif
 /* HEAVY: the scene also has noise / image textures (read from texs through the material, WT_GLOBAL):
- * Perlin turbulence and the image lookup with the sphere's (u, v) are out-of-line calls (tex_heavy,
- * sphere_uv), made only by lanes whose material needs them. */
+ * Perlin turbulence and the sphere's (u, v) are out-of-line calls with by-value arguments (noise_value,
+ * sphere_uv_v), made only by lanes whose material needs them; Perlin tables staged in LDS are read as LDS. */
 template <bool COUNT, int MEM, bool HEAVY = false>
 HRT_LANE_FI bool shade_walk(const KParams& P, const WalkSrc& src, PathState& ps, uint32_t leaf, float closest,
                             Vec3 ro, Vec3 rd, float rtime, float tau, Vec3& sum, Counts& cn) {
