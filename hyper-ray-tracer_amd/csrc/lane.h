@@ -261,6 +261,34 @@ HRT_LANE_FI float4 wload(const WalkSrc& src, uint32_t off) {
   return *reinterpret_cast<const float4*>(src.base + off);
 }
 
+/* Where a walk stream's leaf PAYLOADS are read: a hybrid stream stages node parts only (scene.cpp
+ * walk_place_and_write puts every payload behind them, in global memory), so its payloads are plain
+ * buffer reads, with no per-lane choice between LDS and global memory */
+template <int MEM>
+constexpr int payload_mem() { return MEM == WM_HYB ? WM_BUF : MEM; }
+
+/* Both 16-B halves of the node part at `off` (walk_box).  WM_HYB: every lane issues an LDS read AND a
+ * buffer read of each half, into registers of their own, and keeps one by a select: the LDS lanes' buffer
+ * offset lies beyond the descriptor's range (no memory access; zeros), the global lanes read LDS address 0
+ * (a broadcast).  The per-lane branch of wload<WM_HYB> made the compiler wait for the buffer load before
+ * the LDS read that writes the same registers: two serialised L2 latencies per step. */
+template <int MEM>
+HRT_LANE_FI void wload_node(const WalkSrc& src, uint32_t off, float4& a, float4& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (MEM == WM_HYB) {
+    const bool in_lds = off < src.hot;
+    const uint32_t loff = in_lds ? off : 0u, goff = in_lds ? 0x7FFFFF00u : off;
+    const float4 la = wload<WM_LDS>(src, loff), lb = wload<WM_LDS>(src, loff + 16u);
+    const float4 ga = wload<WM_BUF>(src, goff), gb = wload<WM_BUF>(src, goff + 16u);
+    a = in_lds ? la : ga;
+    b = in_lds ? lb : gb;
+    return;
+  }
+#endif
+  a = wload<MEM>(src, off);
+  b = wload<MEM>(src, off + 16u);
+}
+
 
 /* aabb.rs:20-47 (CULL_REFERENCE), its narrowed form (CULL_SLAB), or CULL_EXACT: the reference test
  * AND an inflated slab test that only rejects boxes no accepted hit can come from (layout.h).
@@ -1028,9 +1056,10 @@ HRT_LANE_FI bool shade(const KParams& P, PathState& ps, uint32_t winner, float c
 /* HEAVY: the scene also has noise / image textures (read from texs through the material, WT_GLOBAL):
  * Perlin turbulence and the sphere's (u, v) are out-of-line calls with by-value arguments (noise_value,
  * sphere_uv_v), made only by lanes whose material needs them; Perlin tables staged in LDS are read as LDS. */
-template <bool COUNT, int MEM, bool HEAVY = false>
+template <bool COUNT, int WMEM, bool HEAVY = false>
 HRT_LANE_FI bool shade_walk(const KParams& P, const WalkSrc& src, PathState& ps, uint32_t leaf, float closest,
                             Vec3 ro, Vec3 rd, float rtime, float tau, Vec3& sum, Counts& cn) {
+  constexpr int MEM = payload_mem<WMEM>();
   if (leaf == G::NONE) { /* a sphere scene's path gathers radiance at its miss only: straight into the sum
                           * (sum + (+0 + thr bg) == sum + thr bg: the sum is never -0) */
     sum = sum + mul_elem(ps.thr, P.background);
@@ -1270,7 +1299,8 @@ HRT_LANE_FI bool box_ce(const float4& a, const float4& b, const TRay& r, float t
  * HEAVY instantiation passes false: at its 128-VGPR cap the three more live registers cost 3% on C3) */
 template <bool COUNT, int MEM, bool FMA = HRT_BOX_FMA && (MEM != WM_HYB || HRT_BOX_FMA_ALL)>
 HRT_LANE_FI void walk_box(const WalkSrc& src, uint32_t& i, const TRay& r, float tmin, float closest, Counts& cn) {
-  const float4 a = wload<MEM>(src, i), b = wload<MEM>(src, i + 16u);
+  float4 a, b;
+  wload_node<MEM>(src, i, a, b);
   uint32_t skip = f2u(a.w);
 #if defined(__HIP_DEVICE_COMPILE__)
   asm("" : "+v"(skip)); /* keep the link in the first 16-B load (see basic_box) */
@@ -1284,9 +1314,10 @@ HRT_LANE_FI void walk_box(const WalkSrc& src, uint32_t& i, const TRay& r, float 
 
 /* The parked leaf's primitive: the reference test on its box (aabb.rs, monotone: leaves suffice, DESIGN
  * section 4), then the sphere test against the lane's closest; the walk continues behind the leaf. */
-template <bool COUNT, int MEM>
+template <bool COUNT, int WMEM>
 HRT_LANE_FI void walk_leaf_test(const KParams& P, const WalkSrc& src, uint32_t leaf, const TRay& r, float& closest,
                                 uint32_t& winner, Counts& cn) {
+  constexpr int MEM = payload_mem<WMEM>();
   const float4 bmn = wload<MEM>(src, leaf), bmx = wload<MEM>(src, leaf + 16u);
   const uint32_t w = f2u(bmn.w);
   if (!(w & G::WL_NOBOX) && !box_ref(bmn, bmx, r, P.t_min, closest)) return;
@@ -1307,7 +1338,7 @@ HRT_LANE_FI void walk_leaf_test(const KParams& P, const WalkSrc& src, uint32_t l
 
 /* the leaf's pre-order successor, kept in its payload (w >> 2) */
 template <int MEM>
-HRT_LANE_FI uint32_t walk_successor(const WalkSrc& src, uint32_t leaf) { return f2u(wload<MEM>(src, leaf).w) >> 2; }
+HRT_LANE_FI uint32_t walk_successor(const WalkSrc& src, uint32_t leaf) { return f2u(wload<payload_mem<MEM>()>(src, leaf).w) >> 2; }
 
 template <bool COUNT, int MEM>
 HRT_LANE_FI void walk_prim(const KParams& P, const WalkSrc& src, uint32_t& i, const TRay& r, float& closest,
@@ -1359,10 +1390,11 @@ HRT_LANE_FI void gwalk_program(const KParams& P, const G::Node* __restrict__ nod
  * (box-less leaves, GL_BOX), then the leaf's program -- its range of the reference stream, whose first
  * node is the leaf's own box (the reference test at the leaf) -- from the world ray
  * against the lane's current closest.  The winner is a reference-stream node index (make_record<true>). */
-template <bool MEDIA, bool COUNT, int MEM>
+template <bool MEDIA, bool COUNT, int WMEM>
 HRT_LANE_FI void gwalk_leaf_test(const KParams& P, const G::Node* __restrict__ nodes, const G::Prim* __restrict__ prims,
                                  const WalkSrc& src, uint32_t leaf, const TRay& r, float& closest, uint32_t& winner,
                                  uint32_t& gstate, const PathKey& pk, Counts& cn) {
+  constexpr int MEM = payload_mem<WMEM>();
   const float4 h = wload<MEM>(src, leaf);
   const uint32_t flags = f2u(h.z);
   /* one call site for the program (the ray: the world ray, or the innermost instance frame's) */

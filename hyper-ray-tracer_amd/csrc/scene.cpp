@@ -786,6 +786,8 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
     }
   }
   s->w_hot = hybrid ? off : 0;
+  /* (the payloads of a hybrid stream all lie behind the staged node parts: lane.h payload_mem reads them
+   * from global memory without a per-lane choice; checked below) */
   for (uint32_t i = 0; i < N; i++) {
     if (!hot[i]) {
       addr[i] = off;
@@ -809,6 +811,9 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
     }
   need(off == total, HRT_ERR_STATE, "walk stream placement");
   const uint32_t END = off;
+  if (s->w_hot)
+    for (uint32_t i = 0; i < N; i++)
+      need(T[i].leaf < 0 || paddr[i] >= s->w_hot, HRT_ERR_STATE, "walk stream: a hybrid stream's payload in its staged part");
   if (!hybrid) s->w_hot = 0;
   std::vector<float>& o = s->w_stream;
   o.assign(END / 4, 0.0f);
