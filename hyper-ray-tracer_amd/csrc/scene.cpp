@@ -1170,6 +1170,8 @@ std::vector<WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<WNode>* ref_t
   };
   const char* flat_env = getenv("HRT_GWALK_FLAT"); /* "0": instance chains stay whole leaf programs (A/B) */
   const bool flat_ok = !(flat_env && strcmp(flat_env, "0") == 0);
+  const char* fl_env = getenv("HRT_GWALK_FLATLIST"); /* "0": a BvhNode leaf's Cuboid / List stays one program (A/B) */
+  const bool flat_lists = !(fl_env && strcmp(fl_env, "0") == 0);
   uint32_t i = 0;
   while (i < n) {
     while (!open.empty() && open.back().end <= i) open.pop_back();
@@ -1197,9 +1199,15 @@ std::vector<WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<WNode>* ref_t
       }
       /* the leaf's single primitive, if the subtree is one world-level prim (for its true extent) */
       std::vector<Flat> fl;
-      bool chains = false;
-      for (uint32_t j = i + 1; j < skip; j++) chains |= ((s->g_nodes[j].kp >> 24) & G::KIND_MASK) == G::K_INST_BEGIN;
-      if (chains && flat_ok && flatten_chains(i + 1, skip, fl) && !fl.empty()) {
+      bool chains = false, prims_only = skip > i + 2;
+      for (uint32_t j = i + 1; j < skip; j++) {
+        const uint32_t kj = (s->g_nodes[j].kp >> 24) & G::KIND_MASK;
+        chains |= kj == G::K_INST_BEGIN;
+        prims_only &= kj == G::K_PRIM;
+      }
+      /* a Cuboid's or a List's box-less primitives under a BvhNode leaf: each its own leaf (its true extent
+       * for the inflated test, the leaf's box tested once per group), as a flattened chain's members */
+      if ((chains || (prims_only && flat_lists)) && flat_ok && flatten_chains(i + 1, skip, fl) && !fl.empty()) {
         /* the BvhNode leaf's box is tested (world frame) before each flattened leaf's program */
         for (size_t q = 0; q < fl.size(); q++) add_flat(fl[q], true, node_box(i), i, q + 1 < fl.size() ? fl[q + 1].begin : skip);
         i = skip;
