@@ -653,6 +653,7 @@ thread_local bool t_has_launch = false;
 /* "void ns::launch_basic(...) [CULL = 2, COUNT = false, ...]" -> "launch_basic[CULL = 2, COUNT = false, ...]" */
 void launch_name(const char* pretty, char* out, size_t cap) {
   std::string s(pretty ? pretty : "?");
+  for (size_t a; (a = s.find("(anonymous namespace)")) != std::string::npos;) s.erase(a, 21);
   const size_t paren = s.find('(');
   std::string head = s.substr(0, paren);
   const size_t sp = head.find_last_of(" :");

@@ -140,6 +140,10 @@ class LaunchInfo(ctypes.Structure):
     ]
 
 
+# Diagnostics an older build may lack; only tolerated when HRT_LIB points at another build (A/B runs)
+OPTIONAL = {"hrt_last_launch", "hrt_debug_box_test"}
+HRT_LIB_OVERRIDE = bool(os.environ.get("HRT_LIB"))
+
 # Every entry point of include/hrt/hrt.h (tests/test_abi.py checks the header against this list).
 EXPORTS = [
     "hrt_last_error", "hrt_version", "hrt_scene_create", "hrt_scene_destroy",
@@ -225,6 +229,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hrt_debug_poke_blob": (S, [vp, u64, vp, u64]),
     }
     for name, (res, args) in sig.items():
+        if name in OPTIONAL and HRT_LIB_OVERRIDE and not hasattr(L, name):
+            continue  # an older build loaded for an A/B run (HRT_LIB): diagnostics it lacks stay unbound
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
