@@ -395,6 +395,38 @@ HRT_LANE_FI bool sphere_root_at(Vec3 c, float radius, const TRay& r, float tmin,
   return true;
 }
 
+/* constant_medium.rs:37-48 on a boundary that is one sphere: boundary.hit(ray, -inf, inf) and then
+ * boundary.hit(ray, t1 + 0.0001, inf) from ONE evaluation of the quadratic (sphere.rs:38-55: oc, half_b,
+ * c, the discriminant, its root and the two candidate roots are the same numbers in both calls; only the
+ * accepted interval differs, and each call's comparisons are made exactly as sphere_root_at makes them).
+ * Returns the number of boundary hits (0, 1 or 2) with t1, t2. */
+HRT_LANE_FI int sphere_pair_at(Vec3 c, float radius, Vec3 o, Vec3 d, float& t1, float& t2) {
+  const float inf = u2f(0x7f800000u);
+  Vec3 oc = o - c;
+  float a = dot(d, d); /* set_dir's r.dd */
+  const float y = div_rn_y(a);
+  float half_b = dot(oc, d);
+  float cc = dot(oc, oc) - radius * radius;
+  float disc = half_b * half_b - a * cc;
+  if (disc < 0.0f) return 0;
+  float sq = sqrtf(disc);
+  const float near = div_rn(-half_b - sq, a, y);
+  float t = near; /* the first call accepts its first root: (t < -inf || inf < t) is false */
+  if (t < -inf || inf < t) {
+    t = div_rn(-half_b + sq, a, y);
+    if (t < -inf || inf < t) return 0;
+  }
+  t1 = t;
+  const float tmin2 = t1 + 0.0001f;
+  t = near;
+  if (t < tmin2 || inf < t) {
+    t = div_rn(-half_b + sq, a, y);
+    if (t < tmin2 || inf < t) return 1;
+  }
+  t2 = t;
+  return 2;
+}
+
 /* sphere.rs:38-55 / moving_sphere.rs:61-78: the accepted root only */
 HRT_LANE_FI bool sphere_root(const G::Prim* pp, uint32_t kind, const TRay& r, float tmin,
                                             float tmax, float& root, bool motion_uniform) {
@@ -525,6 +557,9 @@ struct PathKey {
   uint32_t segment;
 };
 
+#ifndef HRT_MEDIUM_PAIR
+#define HRT_MEDIUM_PAIR 1 /* 0: a one-sphere medium boundary takes the two boundary walks (A/B) */
+#endif
 /* The world walk.  Closest hit over [begin, end) of the node stream with t in [tmin, closest]:
  * `winner` = node index of the accepted leaf (NONE if nothing).  MEDIA: ConstantMedium nodes are
  * evaluated (their boundary walks are nested calls with MEDIA = false). */
@@ -609,11 +644,29 @@ HRT_LANE void trace_ray(const KParams& P, const G::Node* __restrict__ nodes, con
             const G::Medium m = P.media[payload];
             const float inf = u2f(0x7f800000u);
             float c1 = inf, c2 = inf;
-            uint32_t w1 = G::NONE, w2 = G::NONE;
-            trace<CULL, FULL, false, COUNT>(P, nodes, prims, m.bstart, m.bend, r.o, r.d, r.time, -inf, c1, w1, pk, cn);
-            if (w1 == G::NONE) continue;
-            trace<CULL, FULL, false, COUNT>(P, nodes, prims, m.bstart, m.bend, r.o, r.d, r.time, c1 + 0.0001f, c2, w2, pk, cn);
-            if (w2 == G::NONE) continue;
+            if (HRT_MEDIUM_PAIR && m.sphere != G::NONE) { /* one sphere: both queries from one quadratic */
+              const G::Prim* bp = prims + m.sphere;
+              const float4 p0 = ld4(bp->p0);
+              Vec3 c = v3(p0.x, p0.y, p0.z);
+              if ((bp->km & 3u) == G::P_MOVING) { /* moving_sphere.rs:55-58 at the ray's time (set_time) */
+                const float4 p1 = ld4(bp->p1);
+                const float tau = P.motion_uniform ? (r.time - P.motion_t0) / P.motion_span : r.time;
+                const float f = P.motion_uniform ? tau : (tau - p1.w) / bp->p2[0];
+                c = c + f * v3(p1.x, p1.y, p1.z);
+              }
+              const int hits = sphere_pair_at(c, p0.w, r.o, r.d, c1, c2);
+              if constexpr (COUNT) { /* the work counters of the two boundary walks it replaces */
+                cn.nodes += hits > 0 ? 2u : 1u;
+                cn.prims += hits > 0 ? 2u : 1u;
+              }
+              if (hits < 2) continue;
+            } else {
+              uint32_t w1 = G::NONE, w2 = G::NONE;
+              trace<CULL, FULL, false, COUNT>(P, nodes, prims, m.bstart, m.bend, r.o, r.d, r.time, -inf, c1, w1, pk, cn);
+              if (w1 == G::NONE) continue;
+              trace<CULL, FULL, false, COUNT>(P, nodes, prims, m.bstart, m.bend, r.o, r.d, r.time, c1 + 0.0001f, c2, w2, pk, cn);
+              if (w2 == G::NONE) continue;
+            }
             float r1 = c1, r2 = c2;
             if (r1 < tmin) r1 = tmin;
             if (r2 > closest) r2 = closest;

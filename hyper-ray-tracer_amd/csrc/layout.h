@@ -83,7 +83,9 @@ struct alignas(16) Medium {
   uint32_t mat; /* Isotropic phase function */
   uint32_t medium_id;
   uint32_t parent;
-  uint32_t pad0, pad1;
+  uint32_t sphere; /* the boundary is ONE sphere / moving sphere primitive (its prim index), else NONE:
+                      both boundary queries then come from one evaluation of its quadratic (lane.h) */
+  uint32_t pad1;
 };
 
 enum : uint32_t { M_LAMBERTIAN = 0, M_METAL = 1, M_DIELECTRIC = 2, M_DIFFUSE_LIGHT = 3, M_ISOTROPIC = 4 };

@@ -683,6 +683,13 @@ void flatten(hrt_scene* s) {
     f.emit(f.pending[i].boundary, G::NONE);
     s->g_media[f.pending[i].medium].bstart = bstart;
     s->g_media[f.pending[i].medium].bend = (uint32_t)s->g_nodes.size();
+    G::Medium& gm = s->g_media[f.pending[i].medium];
+    gm.sphere = G::NONE;
+    if (gm.bend == gm.bstart + 1) {
+      const uint32_t kp = s->g_nodes[gm.bstart].kp;
+      if (((kp >> 24) & G::KIND_MASK) == G::K_PRIM && (s->g_prims[kp & 0xFFFFFFu].km & 3u) != G::P_RECT)
+        gm.sphere = kp & 0xFFFFFFu;
+    }
   }
   for (const G::Medium& m : s->g_media) s->feature_mask |= tex_features(s, s->g_mats[m.mat].tex);
   /* every instance's chain, outermost first (layout.h CHAIN_F4) */
