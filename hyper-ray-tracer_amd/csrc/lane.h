@@ -198,20 +198,31 @@ HRT_LANE_FI float div_rn(float x, float a, float y) {
   return q;
 }
 
+/* r.noinv from r.o and r.inv, or NaN in all three components (NaN MODE: no inflated culling for this
+ * ray, every inflated test passes; the reference tests still decide).  NaN mode when an inv component is
+ * not a finite normal number or a product is not finite:
+ *  - box_ce's D is exact only for a normal |inv| (a zero or denormal inv drops its axis from D);
+ *  - a direction component of 0 (inv infinite) is also the only way a reference test can accept a NaN t:
+ *    rect.rs:61-70 divides (k - o_k) by d_k, and with the origin ON the rect's plane and the ray parallel to
+ *    it that is 0 / 0; NaN passes `t < t_min || t > t_max` and the bounds checks, so the reference accepts
+ *    a "hit" at t = NaN wherever the rect lies along the ray, beyond the closest hit too (DESIGN G20).  No
+ *    inflated box can hold such a hit, so the walk must not cull for this ray at all. */
+HRT_LANE_FI void set_noinv(TRay& r) {
+  r.noinv = v3(-(r.o.x * r.inv.x), -(r.o.y * r.inv.y), -(r.o.z * r.inv.z));
+  auto normal = [](float x) { return (int)(fabsf(x) >= 0x1p-126f) & (int)(fabsf(x) <= 3.40282347e+38f); }; /* 0 on NaN */
+  auto finite = [](float x) { return (int)(fabsf(x) <= 3.40282347e+38f); };
+  if (!(normal(r.inv.x) & normal(r.inv.y) & normal(r.inv.z) & finite(r.noinv.x) & finite(r.noinv.y) & finite(r.noinv.z)))
+    r.noinv = v3(u2f(0x7fc00000u), u2f(0x7fc00000u), u2f(0x7fc00000u));
+}
+HRT_LANE_FI bool nan_mode(const TRay& r) { return r.noinv.x != r.noinv.x; }
+
 /* a new origin/direction; the ray keeps its time */
 HRT_LANE_FI void set_dir(TRay& r, Vec3 o, Vec3 d) {
   r.o = o;
   r.d = d;
   /* aabb.rs:22 computes 1/d per call; the value is the same every time */
   r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-  r.noinv = v3(-(o.x * r.inv.x), -(o.y * r.inv.y), -(o.z * r.inv.z));
-  /* box_ce's D is exact only for a normal |inv| (a zero or denormal inv drops its axis from D) and a
-   * finite product: otherwise the walk keeps no inflated culling for this ray (the leaves' reference
-   * test still decides) */
-  auto normal = [](float x) { return (int)(fabsf(x) >= 0x1p-126f) & (int)(fabsf(x) <= 3.40282347e+38f); }; /* 0 on NaN */
-  auto finite = [](float x) { return (int)(fabsf(x) <= 3.40282347e+38f); };
-  if (!(normal(r.inv.x) & normal(r.inv.y) & normal(r.inv.z) & finite(r.noinv.x) & finite(r.noinv.y) & finite(r.noinv.z)))
-    r.noinv = v3(u2f(0x7fc00000u), u2f(0x7fc00000u), u2f(0x7fc00000u));
+  set_noinv(r);
   r.dd = dot(d, d);
   r.rdd = div_rn_y(r.dd);
 }
@@ -336,6 +347,10 @@ HRT_LANE_FI bool box_hit(const float4& a, const float4& b, const TRay& r, float 
   bool ok = true; /* the reference: each axis on its own against [t_min, t_max] */
 #pragma unroll
   for (int k = 0; k < 3; k++) ok = ok & !(fminf(te[k], tmax) <= fmaxf(ts[k], tmin));
+  /* aabb.rs:30-36 with a NaN t_max (the closest after a NaN hit, G20) or t_min (a medium's second boundary
+   * walk after a NaN first hit): `if te < t_max {te} else {t_max}` keeps the NaN and `t_max <= t_min` is
+   * false, so every axis passes; fminf / fmaxf would drop the NaN instead */
+  ok = ok | (tmax != tmax) | (tmin != tmin);
   if (CULL == G::CULL_REFERENCE) return ok;
   /* CULL_EXACT: the slab interval widened by margin(box) / |d_k| per axis */
   float dist = 0.0f;
@@ -349,7 +364,7 @@ HRT_LANE_FI bool box_hit(const float4& a, const float4& b, const TRay& r, float 
     lo = fmaxf(lo, ts[k] - w);
     hi = fminf(hi, te[k] + w);
   }
-  return ok & (ref_only | !(hi < lo));
+  return ok & (ref_only | nan_mode(r) | !(hi < lo));
 }
 
 /* The two halves of CULL_EXACT on their own, for the sphere-scene walk (basic_box / basic_prim).
@@ -373,7 +388,7 @@ HRT_LANE_FI bool box_ref(const float4& a, const float4& b, const TRay& r, float 
     const float ts = neg ? t1 : t0, te = neg ? t0 : t1;
     ok = ok & !(fminf(te, tmax) <= fmaxf(ts, tmin));
   }
-  return ok;
+  return ok | (tmax != tmax) | (tmin != tmin); /* a NaN bound passes every axis (box_hit) */
 }
 
 /* sphere.rs:38-55 / moving_sphere.rs:61-78 for a sphere of centre c (at the ray's time) and radius
@@ -528,7 +543,8 @@ HRT_LANE_FI void inst_enter(const G::Inst& in, TRay& r) {
   r.d = nd;
   if (in.kind & G::IF_INV) {
     r.inv = v3(1.0f / nd.x, 1.0f / nd.y, 1.0f / nd.z);
-    }
+    set_noinv(r); /* NaN mode in this frame (box_hit) */
+  }
   if (in.kind & G::IF_DD) {
     r.dd = dot(nd, nd);
     r.rdd = div_rn_y(r.dd);
@@ -545,7 +561,8 @@ HRT_LANE_FI void inst_leave(const KParams& P, const G::Inst& in, TRay& r, Vec3 b
   r.d = nd;
   if (in.kind & G::IF_INV) {
     r.inv = v3(1.0f / nd.x, 1.0f / nd.y, 1.0f / nd.z);
-    }
+    set_noinv(r); /* NaN mode in this frame (box_hit) */
+  }
   if (in.kind & G::IF_DD) {
     r.dd = dot(nd, nd);
     r.rdd = div_rn_y(r.dd);
@@ -1301,7 +1318,9 @@ HRT_LANE_FI void basic_step(const KParams& P, const G::Node* __restrict__ nodes,
 #ifndef HRT_BOX_FMA_ALL
 #define HRT_BOX_FMA_ALL 0 /* 1: the hybrid walk and HEAVY use the fused form too */
 #endif
-template <bool FMA = HRT_BOX_FMA>
+/* NANG: the sub/mul/add form honours the ray's NaN mode (set_noinv; the fused form does by construction).
+ * Only scenes with rects can produce the NaN hits that make it necessary; sphere kernels pass false. */
+template <bool FMA = HRT_BOX_FMA, bool NANG = true>
 HRT_LANE_FI bool box_ce(const float4& a, const float4& b, const TRay& r, float tmin, float tmax) {
   const float C[3] = {a.x, a.y, a.z}, E[3] = {b.x, b.y, b.z};
   const float inv[3] = {r.inv.x, r.inv.y, r.inv.z};
@@ -1344,13 +1363,14 @@ HRT_LANE_FI bool box_ce(const float4& a, const float4& b, const TRay& r, float t
   }
   const float lo = fmaxf(fmaxf(l[0], l[1]), l[2]); /* NaN only if all three are: no constraint */
   const float hi = fminf(fminf(h[0], h[1]), h[2]);
+  if constexpr (!FMA && NANG) return (!(hi < lo) & !(hi < tmin) & !(tmax < lo)) | nan_mode(r);
   return !(hi < lo) & !(hi < tmin) & !(tmax < lo);
 }
 
 /* One node step: an inner node moves to pass / skip; a passed leaf parks the lane on it (WALK_PEND). */
 /* FMA: box_ce's fused form (default except for the latency-bound hybrid walk; the sphere kernel's
  * HEAVY instantiation passes false: at its 128-VGPR cap the three more live registers cost 3% on C3) */
-template <bool COUNT, int MEM, bool FMA = HRT_BOX_FMA && (MEM != WM_HYB || HRT_BOX_FMA_ALL)>
+template <bool COUNT, int MEM, bool FMA = HRT_BOX_FMA && (MEM != WM_HYB || HRT_BOX_FMA_ALL), bool NANG = true>
 HRT_LANE_FI void walk_box(const WalkSrc& src, uint32_t& i, const TRay& r, float tmin, float closest, Counts& cn) {
   float4 a, b;
   wload_node<MEM>(src, i, a, b);
@@ -1362,7 +1382,7 @@ HRT_LANE_FI void walk_box(const WalkSrc& src, uint32_t& i, const TRay& r, float 
 #endif
 #endif
   if constexpr (COUNT) cn.nodes++;
-  i = box_ce<FMA>(a, b, r, tmin, closest) ? f2u(b.w) : skip;
+  i = box_ce<FMA, NANG>(a, b, r, tmin, closest) ? f2u(b.w) : skip;
 }
 
 /* The parked leaf's primitive: the reference test on its box (aabb.rs, monotone: leaves suffice, DESIGN
@@ -1465,7 +1485,10 @@ HRT_LANE_FI void gwalk_leaf_test(const KParams& P, const G::Node* __restrict__ n
        * as the reference's Translation / Rotation hits hand it down (apply_chain), with 1/d and d.d of the
        * turned direction where the program reads them */
       apply_chain(P, f2u(bmn.w), lr.o, lr.d);
-      if (flags & G::GL_INV) lr.inv = v3(1.0f / lr.d.x, 1.0f / lr.d.y, 1.0f / lr.d.z);
+      if (flags & G::GL_INV) {
+        lr.inv = v3(1.0f / lr.d.x, 1.0f / lr.d.y, 1.0f / lr.d.z);
+        set_noinv(lr); /* NaN mode in the innermost frame (box_hit in the program) */
+      }
       if (flags & G::GL_DD) {
         lr.dd = dot(lr.d, lr.d);
         lr.rdd = div_rn_y(lr.dd);

@@ -167,7 +167,16 @@ void render_gwalk_kernel(KParams P) {
         if (pm && ((uint32_t)__popcll(pm) >= batch || !__ballot(node < end))) {
           if constexpr (COUNT) cn.prim_slots++;
           if (pend != G::NONE) {
+            const float before = closest;
             gwalk_leaf_test<MEDIA, COUNT, WMEM>(Q, nodes, prims, ws, pend, r, closest, winner, gstate, ps.pk, cn);
+            if (closest != closest && before == before) {
+              /* the leaf accepted a NaN t (rect.rs 0 / 0, lane.h set_noinv; in an instance's frame the world
+               * ray need not be in NaN mode): the reference now passes every box and accepts the next hit at
+               * any t, but the walk ran ahead culling with the old closest -- walk again from the leaf's
+               * successor (a leaf this lane was blocked on is reached again) */
+              node = walk_successor<WMEM>(ws, pend);
+              pend = G::NONE;
+            }
             pend = G::NONE;
             if (walk_pending(node)) {
               pend = node - WALK_PEND;

@@ -145,7 +145,7 @@ void render_basic_kernel(KParams P) {
       for (int u = 0; u < WALK_UNROLL; u++) {
         if constexpr (COUNT) cn.walk_slots++;
         if (node < end) {
-          if constexpr (WS) walk_box<COUNT, WMEM, HRT_BOX_FMA && ((WMEM != WM_HYB && !HEAVY) || HRT_BOX_FMA_ALL)>(ws, node, r, tmin_c, closest, cn);
+          if constexpr (WS) walk_box<COUNT, WMEM, HRT_BOX_FMA && ((WMEM != WM_HYB && !HEAVY) || HRT_BOX_FMA_ALL), false>(ws, node, r, tmin_c, closest, cn); /* no rects: no NaN hits (lane.h set_noinv) */
           else basic_box<CULL, COUNT, STRIDE>(P, nodes, node, r, closest, cn);
         } else if constexpr (COUNT) {
           if (walk_pending(node)) cn.park_slots++;

@@ -262,3 +262,108 @@ int lane_sim_cull_property(const float* sph, uint32_t n_sph, const float* rays, 
 }
 
 }  // extern "C"
+
+extern "C" {
+/* One path of render_kernel's lane (segment at a time) with culling `cull`: out[9 * k ..] = origin,
+ * direction, time, closest, winner (bits) of segment k; returns the number of segments (diagnostics). */
+int lane_sim_path(const void* blob, const hrt_blob_info* bi, const hrt_camera* cam, const hrt_render_params* p,
+                  int cull, uint32_t px, uint32_t py, uint32_t sample, float* out, uint32_t cap) {
+  std::vector<float> img(4);
+  KParams P;
+  memset(&P, 0, sizeof(P));
+  const uint8_t* base = (const uint8_t*)blob;
+  P.nodes = (const G::Node*)(base + bi->off_nodes);
+  P.prims = (const G::Prim*)(base + bi->off_prims);
+  P.insts = (const G::Inst*)(base + bi->off_insts);
+  P.media = (const G::Medium*)(base + bi->off_media);
+  P.mats = (const G::Mat*)(base + bi->off_mats);
+  P.texs = (const G::Tex*)(base + bi->off_texs);
+  P.perlin = (const G::Perlin*)(base + bi->off_perlin);
+  P.images = base + bi->off_images;
+  P.chains = (const float4*)(base + bi->off_chains);
+  P.main_end = bi->main_end;
+  P.ln_e = bi->ln_e;
+  P.motion_uniform = bi->motion_uniform;
+  P.motion_t0 = bi->motion_t0;
+  P.motion_span = bi->motion_span;
+  P.cam_origin = v3(cam->origin[0], cam->origin[1], cam->origin[2]);
+  P.cam_llc = v3(cam->lower_left_corner[0], cam->lower_left_corner[1], cam->lower_left_corner[2]);
+  P.cam_h = v3(cam->horizontal[0], cam->horizontal[1], cam->horizontal[2]);
+  P.cam_v = v3(cam->vertical[0], cam->vertical[1], cam->vertical[2]);
+  P.cam_u = v3(cam->u[0], cam->u[1], cam->u[2]);
+  P.cam_vv = v3(cam->v[0], cam->v[1], cam->v[2]);
+  P.lens_radius = cam->lens_radius;
+  P.time0 = cam->time0;
+  P.time1 = cam->time1;
+  P.W = p->width;
+  P.H = p->height;
+  set_pixel_rcp(P);
+  P.spp = p->samples;
+  P.max_depth = p->max_depth;
+  P.sample_offset = p->sample_offset;
+  P.t_min = p->t_min;
+  P.background = v3(p->background[0], p->background[1], p->background[2]);
+  P.seed = p->seed;
+  PathState ps;
+  init_path_state(ps);
+  start_sample(P, ps, px, py, sample);
+  Counts cn{0u, 0u, 0u, 0u, 0u, 0u};
+  uint32_t n = 0;
+  float scratch[9];
+  for (;;) {
+    bool done;
+    float* d = n < cap ? out + 9 * n : scratch;
+    if (cull == G::CULL_EXACT) done = segment<G::CULL_EXACT, true, false, false>(P, P.nodes, P.prims, ps, cn, d);
+    else done = segment<G::CULL_REFERENCE, true, false, false>(P, P.nodes, P.prims, ps, cn, d);
+    if (ps.traced) n++;
+    if (done) break;
+  }
+  return (int)n;
+}
+
+/* The reference node stream's box decisions for one ray (o, d, time) over [0, main_end): for each node the
+ * reference test (aabb.rs) and the EXACT test (box_hit<CULL_EXACT>) at the closest the REFERENCE walk has
+ * when it reaches the node; dec[i] bit 0 = visited by the reference walk, bit 1 = reference pass, bit 2 =
+ * exact pass; returns the reference walk's winner (diagnostics). */
+int lane_sim_ray_boxes(const void* blob, const hrt_blob_info* bi, const float* od, float time, float tmin,
+                       uint8_t* dec, float* closest_out) {
+  const uint8_t* base = (const uint8_t*)blob;
+  const G::Node* nodes = (const G::Node*)(base + bi->off_nodes);
+  const G::Prim* prims = (const G::Prim*)(base + bi->off_prims);
+  KParams P;
+  memset(&P, 0, sizeof(P));
+  P.motion_uniform = bi->motion_uniform;
+  P.motion_t0 = bi->motion_t0;
+  P.motion_span = bi->motion_span;
+  TRay r;
+  set_ray(r, v3(od[0], od[1], od[2]), v3(od[3], od[4], od[5]), time, P);
+  float closest = u2f(0x7f800000u);
+  int winner = -1;
+  for (uint32_t i = 0; i < bi->main_end;) {
+    const G::Node* np = nodes + i;
+    const float4 a = ld4(np->mn), b = ld4(np->mx);
+    const uint32_t kp = f2u(b.w), kind = (kp >> 24) & G::KIND_MASK, payload = kp & 0xFFFFFFu;
+    dec[i] |= 1;
+    if (kind == G::K_BOX || kind == G::K_BOX_PRIM) {
+      const bool ref = box_hit<G::CULL_REFERENCE>(a, b, r, tmin, closest);
+      const bool ex = box_hit<G::CULL_EXACT>(a, b, r, tmin, closest, (kp & G::NODE_REF_ONLY) != 0);
+      dec[i] |= (ref ? 2 : 0) | (ex ? 4 : 0);
+      if (kind == G::K_BOX) { i = ref ? i + 1 : f2u(a.w); continue; }
+      i++;
+      if (!ref) continue;
+    } else if (kind == G::K_PRIM) {
+      i++;
+    } else {
+      return -2; /* instances / media: not handled here */
+    }
+    const G::Prim* pp = prims + payload;
+    float t;
+    bool h;
+    if ((pp->km & 3u) == G::P_RECT) h = rect_t(pp, (pp->km >> 2) & 3u, r, tmin, closest, t);
+    else h = sphere_root(pp, pp->km & 3u, r, tmin, closest, t, P.motion_uniform != 0);
+    if (h) { closest = t; winner = (int)(i - 1); }
+  }
+  *closest_out = closest;
+  return winner;
+}
+}  // extern "C"

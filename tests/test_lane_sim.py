@@ -32,12 +32,11 @@ BASIC_SCENES = {"random", "two_spheres", "random_10k", "motion"}
 HEAVY_SPHERE_SCENES = {"earth", "two_perlin_spheres", "earth_perlin"}
 
 
-@pytest.fixture(scope="module")
-def sim(tmp_path_factory):
+def _build_sim(tmp_path_factory, extra=()):
     so = str(tmp_path_factory.mktemp("lanesim") / "liblanesim.so")
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     subprocess.run([hipcc, "-O2", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
-                    "--offload-host-only", "-I" + os.path.join(ROOT, "include"),
+                    "--offload-host-only", *extra, "-I" + os.path.join(ROOT, "include"),
                     "-I" + os.path.join(ROOT, "hyper-ray-tracer_amd", "csrc"),
                     os.path.join(HERE, "native", "lane_sim.hip"), "-o", so], check=True)
     L = ctypes.CDLL(so)
@@ -45,6 +44,18 @@ def sim(tmp_path_factory):
     L.lane_sim_chunks.restype = ctypes.c_int
     L.lane_sim_chunks.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32]
     return L
+
+
+@pytest.fixture(scope="module")
+def sim(tmp_path_factory):
+    return _build_sim(tmp_path_factory)
+
+
+@pytest.fixture(scope="module")
+def sim_submuladd(tmp_path_factory):
+    """The lanes with the walk's sub/mul/add box form everywhere (HRT_BOX_FMA=0: the form hybrid general
+    streams use, and the one r03's general kernel diverged with)."""
+    return _build_sim(tmp_path_factory, ("-DHRT_BOX_FMA=0",))
 
 
 def sim_render(L, name, w, h, spp, depth, seed, earth, kernel, cull, region=None, sample_offset=0, t_min=0.001):
@@ -346,3 +357,47 @@ def test_custom_scenes_exact_lanes_equal_reference_traversal(sim):
         assert sa["nodes"] < sb["nodes"]
     rc, _, _ = sim_render_scene(sim, scenes.sphere_lists(), 8, 8, 1, 0, CULL_EXACT)
     assert rc == 1  # no sphere stream: the sphere kernel's lane must not run it
+
+
+# (x, y, sample) of Cornell 2048^2 (C5) whose paths meet a NaN hit (DESIGN G20: rect.rs divides 0 by 0 for a
+# ray that starts on a rect's plane parallel to it, and accepts t = NaN); found by scripts/box_hunt.py on
+# C5's 1/8 share at 10000 spp, where the r03 kernels left the oracle's path
+NAN_HIT_SAMPLES = [(1644, 1582, 3973), (1574, 232, 8326), (410, 250, 4811)]
+
+
+@pytest.mark.parametrize("form", ["fused", "submuladd"])
+@pytest.mark.parametrize("x,y,sample", NAN_HIT_SAMPLES)
+def test_nan_hit_paths_match_oracle(sim, sim_submuladd, earth, x, y, sample, form):
+    """After a NaN hit the reference passes every box (aabb.rs: `t_max <= t_min` is false for a NaN t_max) and
+    accepts the next hit at any t; the lanes' reference test must keep that (no fminf dropping the NaN), and
+    EXACT culling must not cull for a ray that can meet a NaN hit (set_noinv's NaN mode): every lane, both
+    culling modes, the oracle's world.hit count; the first sample is the one whose path is all NaN hits."""
+    W = H = 2048
+    lanes = sim if form == "fused" else sim_submuladd
+    ref, cnt = oracle_render("cornell", W, H, 1, 50, 1, earth, region=(x, y, 1, 1), sample_offset=sample)
+    for kernel, cull in ((3, CULL_EXACT), (1, CULL_EXACT), (2, CULL_EXACT), (2, CULL_REFERENCE), (1, CULL_REFERENCE)):
+        img, st = sim_render(lanes, "cornell", W, H, 1, 50, 1, earth, kernel=kernel, cull=cull, region=(x, y, 1, 1),
+                             sample_offset=sample)
+        assert st["segments"] == cnt["segments"], (kernel, cull, st["segments"], cnt["segments"])
+        assert np.array_equal(img, ref, equal_nan=True) or np.abs(img - ref).max() <= TOL, (kernel, cull, img, ref)
+
+
+def test_nan_hit_path_is_all_nan(sim, earth):
+    """The first sample's path: segment 3 starts on the floor (y = 0) with a direction whose y component is 0
+    (a Lambertian scatter whose unit vector rounds to the normal's opposite), so the floor's test gives 0 / 0;
+    every later segment starts at a NaN point and meets NaN hits again, up to the depth cap."""
+    W = H = 2048
+    s = hrt.preset("cornell", 1, earth)
+    blob, info = hrt.scene_blob(s)
+    cam = hrt.preset_camera(s.info, W, H)
+    p = hrt.params(W, H, 1, 50, 1, tuple(s.info.background))
+    fn = sim.lane_sim_path
+    fn.restype = ctypes.c_int
+    out = np.zeros(9 * 64, np.float32)
+    for cull in (CULL_EXACT, CULL_REFERENCE):
+        n = fn(blob, ctypes.byref(info), ctypes.byref(cam), ctypes.byref(p), cull, 1644, 1582, 3973,
+               out.ctypes.data_as(ctypes.c_void_p), 64)
+        seg = out[:9 * n].reshape(n, 9)
+        assert n == 50
+        assert seg[3, 1] == 0.0 and seg[3, 4] == 0.0 and np.isnan(seg[3, 7])  # o.y = 0, d.y = 0, t = NaN
+        assert np.isnan(seg[4:, 0]).all()
