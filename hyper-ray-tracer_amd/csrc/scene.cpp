@@ -591,8 +591,68 @@ Aabb box_union(const Aabb& a, const Aabb& b) {
   return u;
 }
 
+/* Optimal re-grouping of a fixed leaf sequence by dynamic programming (HRT_WALK_DP = 1 | 2, n <= 2048):
+ * cost(i, j) = w(i, j) + min_k cost(i, k) + cost(k, j) over the ranges of the sequence, with w = 2 x the half
+ * area (mode 1: the two child tests an inner node makes whenever a ray passes it) or half area x leaves
+ * (mode 2: walk_regroup's greedy objective, minimised exactly).  Splits tie to the cut nearest the middle. */
+bool walk_regroup_dp(std::vector<WNode>& T, const std::vector<WalkLeaf>& leaves, int mode) {
+  const uint32_t n = (uint32_t)leaves.size();
+  if (n < 2 || n > 2048) return false;
+  std::vector<double> A((size_t)n * (n + 1), 0.0), C((size_t)n * (n + 1), 0.0);
+  std::vector<uint32_t> K((size_t)n * (n + 1), 0u);
+  std::vector<Aabb> box((size_t)n * (n + 1));
+  auto at = [n](uint32_t i, uint32_t j) { return (size_t)i * (n + 1) + j; };
+  for (uint32_t i = 0; i < n; i++) {
+    Aabb u = leaves[i].box;
+    box[at(i, i + 1)] = u;
+    A[at(i, i + 1)] = half_area(u);
+    for (uint32_t j = i + 2; j <= n; j++) {
+      u = box_union(u, leaves[j - 1].box);
+      box[at(i, j)] = u;
+      A[at(i, j)] = half_area(u);
+    }
+  }
+  for (uint32_t len = 2; len <= n; len++)
+    for (uint32_t i = 0; i + len <= n; i++) {
+      const uint32_t j = i + len, mid = i + len / 2;
+      double best = HUGE_VAL;
+      uint32_t bk = mid;
+      for (uint32_t k = i + 1; k < j; k++) {
+        const double c = C[at(i, k)] + C[at(k, j)];
+        const uint32_t dk = k > mid ? k - mid : mid - k, db = bk > mid ? bk - mid : mid - bk;
+        if (c < best || (c == best && dk < db)) {
+          best = c;
+          bk = k;
+        }
+      }
+      C[at(i, j)] = best + (mode == 2 ? A[at(i, j)] * len : 2.0 * A[at(i, j)]);
+      K[at(i, j)] = bk;
+    }
+  struct Range { uint32_t lo, hi, depth; };
+  std::vector<Range> todo{{0u, n, 0u}};
+  while (!todo.empty()) {
+    const Range r = todo.back();
+    todo.pop_back();
+    const uint32_t m = r.hi - r.lo, self = (uint32_t)T.size();
+    if (m == 1) {
+      T.push_back(WNode{leaves[r.lo].box, (int32_t)r.lo, self + 1, r.depth});
+      continue;
+    }
+    const uint32_t k = K[at(r.lo, r.hi)];
+    T.push_back(WNode{box[at(r.lo, r.hi)], -1, self + 2 * m - 1, r.depth});
+    todo.push_back({k, r.hi, r.depth + 1});
+    todo.push_back({r.lo, k, r.depth + 1});
+  }
+  return true;
+}
+
 /* re-grouped hierarchy over leaves[0, n), iterative, pre-order (a range of n leaves is 2n - 1 nodes) */
 void walk_regroup(std::vector<WNode>& T, const std::vector<WalkLeaf>& leaves) {
+  /* default: the DP (mode 1) for sequences of at most 700 leaves (O(n^3 / 6) work: ~30 ms at Random's 485),
+   * the greedy split above that (and on the device, build_walk.hip) */
+  const char* dp = getenv("HRT_WALK_DP");
+  const int mode = dp ? dp[0] - '0' : (leaves.size() <= 700 ? 1 : 0);
+  if ((mode == 1 || mode == 2) && walk_regroup_dp(T, leaves, mode)) return;
   struct Range { uint32_t lo, hi, depth; };
   std::vector<Range> todo{{0u, (uint32_t)leaves.size(), 0u}};
   std::vector<Aabb> pre, suf;

@@ -18,6 +18,7 @@ def _walk_bytes(s):
 
 def _committed(build, monkeypatch, make):
     monkeypatch.setenv("HRT_WALK_BUILD", build)
+    monkeypatch.setenv("HRT_WALK_DP", "0")  # the host's greedy split, which the device build mirrors
     s = make()
     s.commit()
     monkeypatch.delenv("HRT_WALK_BUILD")
