@@ -278,6 +278,10 @@ HRT_LANE_FI float4 wload(const WalkSrc& src, uint32_t off) {
 template <int MEM>
 constexpr int payload_mem() { return MEM == WM_HYB ? WM_BUF : MEM; }
 
+#ifndef HRT_HYB_ANYG
+#define HRT_HYB_ANYG 1 /* skip the buffer loads of a step when every lane of the wave reads LDS (r04: C4 1/8 share
+                          * 5291 -> 5424 Mrays/s at 256 spp, A/B on one box; 0 for A/B) */
+#endif
 /* Both 16-B halves of the node part at `off` (walk_box).  WM_HYB: every lane issues an LDS read AND a
  * buffer read of each half, into registers of their own, and keeps one by a select: the LDS lanes' buffer
  * offset lies beyond the descriptor's range (no memory access; zeros), the global lanes read LDS address 0
@@ -290,7 +294,16 @@ HRT_LANE_FI void wload_node(const WalkSrc& src, uint32_t off, float4& a, float4&
     const bool in_lds = off < src.hot;
     const uint32_t loff = in_lds ? off : 0u, goff = in_lds ? 0x7FFFFF00u : off;
     const float4 la = wload<WM_LDS>(src, loff), lb = wload<WM_LDS>(src, loff + 16u);
+#if HRT_HYB_ANYG
+    /* the buffer loads only when a lane of the wave needs them (a wave-uniform branch) */
+    float4 ga = make_float4(0.0f, 0.0f, 0.0f, 0.0f), gb = ga;
+    if (__builtin_amdgcn_ballot_w64(!in_lds)) {
+      ga = wload<WM_BUF>(src, goff);
+      gb = wload<WM_BUF>(src, goff + 16u);
+    }
+#else
     const float4 ga = wload<WM_BUF>(src, goff), gb = wload<WM_BUF>(src, goff + 16u);
+#endif
     a = in_lds ? la : ga;
     b = in_lds ? lb : gb;
     return;
@@ -1361,10 +1374,14 @@ HRT_LANE_FI bool box_ce(const float4& a, const float4& b, const TRay& r, float t
     l[k] = fmaf(-t, fabsf(inv[k]), m[k]);
     h[k] = fmaf(t, fabsf(inv[k]), m[k]);
   }
-  const float lo = fmaxf(fmaxf(l[0], l[1]), l[2]); /* NaN only if all three are: no constraint */
-  const float hi = fminf(fminf(h[0], h[1]), h[2]);
-  if constexpr (!FMA && NANG) return (!(hi < lo) & !(hi < tmin) & !(tmax < lo)) | nan_mode(r);
-  return !(hi < lo) & !(hi < tmin) & !(tmax < lo);
+  /* max(lo, tmin) <= min(hi, tmax) is !(hi < lo) & !(hi < tmin) & !(tmax < lo) when tmin <= tmax (a walk's
+   * closest never drops below t_min; a NaN closest, G20, leaves min(hi, NaN) = hi: no bound from it, as the
+   * three-comparison form) -- one comparison and no mask arithmetic.  A NaN lo / hi (all three axes NaN) is
+   * no constraint either way. */
+  const float lo = fmaxf(fmaxf(fmaxf(l[0], l[1]), l[2]), tmin);
+  const float hi = fminf(fminf(fminf(h[0], h[1]), h[2]), tmax);
+  if constexpr (!FMA && NANG) return !(hi < lo) | nan_mode(r);
+  return !(hi < lo);
 }
 
 /* One node step: an inner node moves to pass / skip; a passed leaf parks the lane on it (WALK_PEND). */

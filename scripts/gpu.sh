@@ -74,7 +74,7 @@ step() {
   case $kind in
     tests)
       if [ $# -gt 0 ]; then run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread -p no:cacheprovider -k "$*"
-      else run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread -p no:cacheprovider; fi ;;
+      else run tests 900 python -u -m pytest tests -m gpu -x -v --durations=25 --timeout 200 --timeout-method thread -p no:cacheprovider; fi ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) local tag=$1; shift; bench_line "$tag" 600 "$@" ;;
     rehearsal)

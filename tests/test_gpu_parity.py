@@ -266,12 +266,14 @@ def test_general_walk_watchdog(earth):
     assert info.walk_bytes > 0
     ws = np.frombuffer(buf.raw, np.uint32, count=info.walk_bytes // 4, offset=info.off_walk).copy()
     off, inner = 0, 0
-    while off < info.walk_bytes:
-        leaf = (ws[off // 4 + 7] & 0x80000000) != 0
-        if not leaf:
+    while off < info.walk_bytes:  # pre-order over the node parts by their links (records may be placed apart)
+        link, skip = int(ws[off // 4 + 7]), int(ws[off // 4 + 3])
+        if link & 0x80000000:  # a leaf: its pass link is its payload; the walk goes on at its skip link
+            off = skip
+        else:
             ws[off // 4 + 3] = 0
             inner += 1
-        off += 80 if leaf else 32  # layout.h WALK_NODE_BYTES (+ GWALK_PAYLOAD_BYTES)
+            off = link
     assert inner > 100
     s.poke_blob(info.off_walk, ws.tobytes())
     with pytest.raises(hrt.HrtError) as e:
