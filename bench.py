@@ -294,9 +294,11 @@ def delivery_phase(args, scene, cam, p, tiles, n_px, dev, stream, world, rank, b
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t[0])
         scene.synchronize()
-    finally:
-        barrier()
-        fd.close()
+    except BaseException:
+        fd.close(failed=True)  # no collective on the error path: the other ranks' waits end on the shared flag
+        raise
+    barrier()
+    fd.close()
     frame_ms = dt / K * 1e3
     d = {"frame_ms": round(frame_ms, 2), "ms_per_step": round(ms_per_step, 2),
          "frame_vs_launch": round(frame_ms / max(1e-9, ms_per_step), 4), "frames": K,

@@ -150,9 +150,24 @@ class FrameDelivery:
         if self.err:
             raise self.err
 
-    def close(self) -> None:
+    def close(self, failed: bool = False) -> None:
+        """Stop the worker and release the segment.  failed=True (an error on this rank): raise the shared
+        error flag first, so that this worker's and every other rank's waits end instead of running into
+        WAIT_S.  A worker still blocked after the join keeps its views of the segment: the segment is then
+        left to the OS (closing it under live views would raise BufferError and hide the first error)."""
+        if failed or self.err is not None:
+            try:
+                self.hdr[self.world + 1] = 1
+            except Exception:
+                pass
         self.q.put(None)
         self.worker.join(timeout=30)
+        if self.worker.is_alive():
+            import sys
+
+            print(f"[delivery rank {self.rank}] worker still running at close; shared frame left open",
+                  file=sys.stderr, flush=True)
+            return
         del self.hdr, self.frames
         self.shm.close()
         if self.rank == 0:

@@ -14,7 +14,13 @@ from oracle import oracle as O
 TOL = 1e-3
 
 # (preset, width, height, spp, depth): every scene feature of the reference; spp > 16 on sphere scenes
-# and spp > 32 on general ones exercises the sample-chunk split (chunk sums reduced in a fixed order)
+# and spp > 32 on general ones exercises the sample-chunk split (chunk sums reduced in a fixed order).
+# earth_perlin, random_10k, features and motion are BUILD-DEFINED scenes (no reference builder): the oracle
+# builds them with the same generator as the library, so their cases check the kernels against the
+# restatement of the reference's per-object code, and no reference fixture covers them (parity unpinned,
+# like every scene here: the reference has no fixtures at all).  The per-sphere shutter
+# path of `motion` (the ray's time in TRay.tau) is also held to the uniform-motion path of the reference
+# scenes indirectly: Random's moving spheres run the scene-wide factor, `motion` the per-sphere one.
 CASES = [
     ("random", 40, 24, 100, 50),
     ("cornell", 24, 24, 70, 50),

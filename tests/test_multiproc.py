@@ -144,3 +144,48 @@ def test_split_is_a_balanced_partition(world):
         for band in range(0, Hf, 128):
             n = sum(1 for t in p if band <= t[1] < band + 128)
             assert abs(n - len([t for t in allt if band <= t[1] < band + 128]) / world) <= 8
+
+
+def _failing_delivery_worker(rank, world, port, q):
+    """Rank 1 fails before its first share (as if its launch raised) and closes its delivery with failed=True;
+    rank 0, waiting for that share, must end with an error soon (not after delivery.WAIT_S), and closing
+    must not raise."""
+    import sys
+    import time
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "hyper-ray-tracer_amd"), root]
+    from hrt import delivery, tiling
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tiles = tiling.split_tiles(W, H, world, rank, 16)
+    fd = delivery.FrameDelivery(W, H, world, rank, tiles)
+    dist.barrier()
+    t0 = time.perf_counter()
+    err = None
+    if rank == 1:
+        fd.close(failed=True)
+    else:
+        fd.submit(0, np.zeros(tiling.share_pixels(tiles) * 4, np.float32))
+        try:
+            fd.flush(1)
+        except RuntimeError as e:
+            err = str(e)
+        fd.close(failed=err is not None)
+        q.put((err, time.perf_counter() - t0))
+    dist.destroy_process_group()
+
+
+def test_delivery_error_path_ends_every_rank():
+    """an error on one rank must not leave the others waiting on the shared frame (the shared
+    error flag ends their waits) nor hide the first error behind a BufferError at close."""
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    pc = mp.start_processes(_failing_delivery_worker, args=(2, _free_port(), q), nprocs=2, join=False,
+                            start_method="spawn")
+    err, dt = q.get()
+    while not pc.join(timeout=60):
+        pass
+    assert err is not None and "failed" in err
+    assert dt < 30
