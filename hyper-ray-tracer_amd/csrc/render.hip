@@ -579,8 +579,12 @@ KParams scene_params(const hrt_scene* s, const hrt_camera* cam, const hrt_render
    * of postpone {40..56} x batch {4, 6, 8}: C2 best at 52-56 / 4, random-10k at 44 / 4, +1.8% over 48 / 6;
    * DESIGN.md section 10) */
   const bool spec = !pl.full && !pl.general && !pl.fast && pl.cull == G::CULL_EXACT;
-  kp.postpone = env_knob("HRT_POSTPONE", pl.gwalk ? 44 : (spec ? (s->w_hot ? 44 : 52) : 56));
-  kp.prim_batch = env_knob("HRT_PRIM_BATCH", pl.gwalk ? 32 : (spec ? 4 : 8)); /* gwalk: r03d sweep, Cornell 4 / 8 / 16 / 32 = 9496 / 9838 / 10271 / 10474 */
+  /* gwalk (r04 sweeps, one box): streams in LDS (Cornell 1/8 share, 1250 spp) batch 16 / 32 = 14183 / 14014;
+   * deep streams staged in part (Final 800^2 x 64: many leaf programs per ray) batch 32 / 16 / 8 / 4 = 1258 /
+   * 1373 / 1430 / 1389, postpone 52 / 44 / 32 = 1131 / 1188 / 1385 (batch 32) */
+  const bool deep = pl.gwalk && pl.gwalk_mem != WM_LDS;
+  kp.postpone = env_knob("HRT_POSTPONE", pl.gwalk ? (deep ? 32 : 44) : (spec ? (s->w_hot ? 44 : 52) : 56));
+  kp.prim_batch = env_knob("HRT_PRIM_BATCH", pl.gwalk ? (deep ? 8 : 16) : (spec ? 4 : 8));
   /* a walk visits each node at most once, a medium's boundary subtree at most twice per medium node */
   kp.walk_cap = 3u * (uint32_t)s->g_nodes.size() + 64u;
   kp.motion_uniform = s->motion_uniform ? 1u : 0u;
