@@ -87,6 +87,7 @@ struct KParams {
   uint32_t n_insts, n_media, n_mats, n_texs; /* record counts (render_gwalk_kernel stages them in LDS) */
   uint32_t n_perlin;   /* Perlin tables (7 KB each); perlin_lds: the kernel stages them in LDS */
   uint32_t perlin_lds;
+  uint32_t walk_half;  /* the walk stream's node-part split (layout.h WALK_SPLIT_HALF) or 16 */
 };
 
 /* Sample-chunk size: spp <= cmin keeps one work item per pixel (the reference's sequential sum), larger
@@ -249,6 +250,8 @@ enum : int { WM_LDS = 0, WM_BUF = 1, WM_HOST = 2, WM_HYB = 3 /* LDS below `hot`,
 struct WalkSrc {
   const uint8_t* base; /* WM_BUF: the section in global memory; WM_HOST: the host copy */
   uint32_t hot;        /* WM_HYB */
+  uint32_t half = 16;  /* WM_HOST: bytes from a node part's first 16 B to its second (the kernels: a template
+                          constant, layout.h WALK_SPLIT_HALF or 16) */
 #if defined(__HIP_DEVICE_COMPILE__)
   __amdgpu_buffer_rsrc_t rsrc; /* WM_BUF */
 #endif
@@ -287,7 +290,7 @@ constexpr int payload_mem() { return MEM == WM_HYB ? WM_BUF : MEM; }
  * offset lies beyond the descriptor's range (no memory access; zeros), the global lanes read LDS address 0
  * (a broadcast).  The per-lane branch of wload<WM_HYB> made the compiler wait for the buffer load before
  * the LDS read that writes the same registers: two serialised L2 latencies per step. */
-template <int MEM>
+template <int MEM, uint32_t HALF = 16>
 HRT_LANE_FI void wload_node(const WalkSrc& src, uint32_t off, float4& a, float4& b) {
 #if defined(__HIP_DEVICE_COMPILE__)
   if constexpr (MEM == WM_HYB) {
@@ -317,7 +320,7 @@ HRT_LANE_FI void wload_node(const WalkSrc& src, uint32_t off, float4& a, float4&
   }
 #endif
   a = wload<MEM>(src, off);
-  b = wload<MEM>(src, off + 16u);
+  b = wload<MEM>(src, off + (MEM == WM_HOST ? src.half : HALF));
 }
 
 
@@ -1394,10 +1397,11 @@ HRT_LANE_FI bool box_ce(const float4& a, const float4& b, const TRay& r, float t
 /* One node step: an inner node moves to pass / skip; a passed leaf parks the lane on it (WALK_PEND). */
 /* FMA: box_ce's fused form (default except for the latency-bound hybrid walk; the sphere kernel's
  * HEAVY instantiation passes false: at its 128-VGPR cap the three more live registers cost 3% on C3) */
-template <bool COUNT, int MEM, bool FMA = HRT_BOX_FMA && (MEM != WM_HYB || HRT_BOX_FMA_ALL), bool NANG = true>
+template <bool COUNT, int MEM, bool FMA = HRT_BOX_FMA && (MEM != WM_HYB || HRT_BOX_FMA_ALL), bool NANG = true,
+          uint32_t HALF = 16>
 HRT_LANE_FI void walk_box(const WalkSrc& src, uint32_t& i, const TRay& r, float tmin, float closest, Counts& cn) {
   float4 a, b;
-  wload_node<MEM>(src, i, a, b);
+  wload_node<MEM, HALF>(src, i, a, b);
   uint32_t skip = f2u(a.w);
 #if defined(__HIP_DEVICE_COMPILE__)
   asm("" : "+v"(skip)); /* keep the link in the first 16-B load (see basic_box) */

@@ -197,6 +197,12 @@ constexpr uint32_t WALK_PEND = 1u << 31;
 constexpr uint32_t LDS_SCENE_MAX_BYTES = 77u * 1024u;
 static_assert(2u * (LDS_SCENE_MAX_BYTES + 768u * 4u) <= 160u * 1024u, "two sphere workgroups per CU");
 constexpr uint32_t WALK_NODE_BYTES = 32, WALK_PAYLOAD_BYTES = 96;
+/* Split node parts (r04, sphere streams staged whole in LDS): a node part's first 16 B (C, skip) at its
+ * offset, its second 16 B (E, pass) WALK_SPLIT_HALF bytes further (an immediate offset of the LDS read),
+ * so consecutive node parts lie 16 B apart in each half and a 16-lane group of ds_read_b128 spreads over
+ * all 16 bank slots (interleaved 32-B parts use 8).  Node parts then occupy [0, 16 N) and
+ * [WALK_SPLIT_HALF, WALK_SPLIT_HALF + 16 N); payloads fill the rest (N <= 1024). */
+constexpr uint32_t WALK_SPLIT_HALF = 16384;
 constexpr uint32_t WL_MOVING = 1u, WL_NOBOX = 2u;
 enum : uint32_t { WT_SOLID = 0, WT_CHECKER = 1, WT_GLOBAL = 2 }; /* inline texture of a leaf's material */
 

@@ -595,6 +595,7 @@ KParams scene_params(const hrt_scene* s, const hrt_camera* cam, const hrt_render
   kp.walk_end = s->w_end;
   kp.walk_hot = (pl.gwalk && pl.gwalk_mem == WM_HYB) || (pl.lds && !pl.full && !pl.fast && pl.cull == G::CULL_EXACT)
                     ? s->w_hot : 0;
+  kp.walk_half = s->w_half;
   return kp;
 }
 

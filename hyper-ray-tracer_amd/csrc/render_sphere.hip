@@ -25,7 +25,8 @@ constexpr int sphere_waves() { return HEAVY ? HRT_HEAVY_WAVES : BASIC_WAVES; }
 
 /* HYB (CULL_EXACT with LDS): the walk stream exceeds the LDS budget; its first P.walk_hot bytes (the
  * hierarchy's top levels) are staged, the rest is read through the buffer descriptor (layout.h) */
-template <int CULL, bool COUNT, bool LDS, bool HYB = false, bool HEAVY = false>
+/* SPLIT: the stream's node parts are split (layout.h WALK_SPLIT_HALF; LDS, not HYB) */
+template <int CULL, bool COUNT, bool LDS, bool HYB = false, bool HEAVY = false, bool SPLIT = false>
 __global__ __launch_bounds__((basic_block_threads<LDS, sphere_waves<HEAVY>()>()), sphere_waves<HEAVY>())
 void render_basic_kernel(KParams P) {
   extern __shared__ float4 lds_scene[];
@@ -145,7 +146,8 @@ void render_basic_kernel(KParams P) {
       for (int u = 0; u < WALK_UNROLL; u++) {
         if constexpr (COUNT) cn.walk_slots++;
         if (node < end) {
-          if constexpr (WS) walk_box<COUNT, WMEM, HRT_BOX_FMA && ((WMEM != WM_HYB && !HEAVY) || HRT_BOX_FMA_ALL), false>(ws, node, r, tmin_c, closest, cn); /* no rects: no NaN hits (lane.h set_noinv) */
+          if constexpr (WS) walk_box<COUNT, WMEM, HRT_BOX_FMA && ((WMEM != WM_HYB && !HEAVY) || HRT_BOX_FMA_ALL), false,
+                                    SPLIT ? G::WALK_SPLIT_HALF : 16u>(ws, node, r, tmin_c, closest, cn); /* no rects: no NaN hits (lane.h set_noinv) */
           else basic_box<CULL, COUNT, STRIDE>(P, nodes, node, r, closest, cn);
         } else if constexpr (COUNT) {
           if (walk_pending(node)) cn.park_slots++;
@@ -246,9 +248,9 @@ void render_basic_kernel(KParams P) {
 }
 
 
-template <int CULL, bool COUNT, bool LDS, bool HYB = false, bool HEAVY = false>
+template <int CULL, bool COUNT, bool LDS, bool HYB = false, bool HEAVY = false, bool SPLIT = false>
 void launch_basic(const KParams& kp, int device, hipStream_t stream, size_t smem) {
-  const void* fn = (const void*)render_basic_kernel<CULL, COUNT, LDS, HYB, HEAVY>;
+  const void* fn = (const void*)render_basic_kernel<CULL, COUNT, LDS, HYB, HEAVY, SPLIT>;
   const int block = basic_block_threads<LDS, sphere_waves<HEAVY>()>();
   /* LDS: the staged scene, then one u32 result slot per thread (layout.h LDS_SCENE_MAX_BYTES leaves
    * room for both, twice per CU) */
@@ -256,7 +258,7 @@ void launch_basic(const KParams& kp, int device, hipStream_t stream, size_t smem
   p.lane_lds = LDS ? (uint32_t)((smem + 15) & ~(size_t)15) : 0u;
   const size_t total = p.lane_lds + (size_t)block * sizeof(uint32_t);
   const int grid = resident_grid(fn, block, device, total, true, __PRETTY_FUNCTION__);
-  hipLaunchKernelGGL((render_basic_kernel<CULL, COUNT, LDS, HYB, HEAVY>), dim3(grid), dim3(block), total, stream, p);
+  hipLaunchKernelGGL((render_basic_kernel<CULL, COUNT, LDS, HYB, HEAVY, SPLIT>), dim3(grid), dim3(block), total, stream, p);
   hip_check(hipGetLastError(), "render_basic_kernel launch");
 }
 
@@ -282,6 +284,11 @@ void launch_sphere(int cull, bool count, bool lds, bool heavy, const KParams& kp
   if (cull == G::CULL_EXACT && lds && kp.walk_hot > 0) { /* top levels in LDS, the rest in global memory */
     if (count) launch_basic<G::CULL_EXACT, true, true, true>(kp, device, stream, smem);
     else launch_basic<G::CULL_EXACT, false, true, true>(kp, device, stream, smem);
+  } else if (cull == G::CULL_EXACT && kp.walk_half != 16u) { /* split node parts (layout.h; F_BASIC scenes) */
+    if (count) lds ? launch_basic<G::CULL_EXACT, true, true, false, false, true>(kp, device, stream, smem)
+                   : launch_basic<G::CULL_EXACT, true, false, false, false, true>(kp, device, stream, 0);
+    else lds ? launch_basic<G::CULL_EXACT, false, true, false, false, true>(kp, device, stream, smem)
+             : launch_basic<G::CULL_EXACT, false, false, false, false, true>(kp, device, stream, 0);
   } else if (cull == G::CULL_EXACT) {
     if (count) lds ? launch_basic<G::CULL_EXACT, true, true>(kp, device, stream, smem)
                    : launch_basic<G::CULL_EXACT, true, false>(kp, device, stream, 0);

@@ -877,7 +877,29 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
       off += PB;
     }
   need(off == total, HRT_ERR_STATE, "walk stream placement");
-  const uint32_t END = off;
+  uint32_t END = off;
+  /* split node parts (layout.h WALK_SPLIT_HALF): sphere streams staged whole in LDS that fill the space
+   * between the two halves with payloads (HRT_WALK_SPLIT=0 keeps 32-B parts) */
+  const char* sp_env = getenv("HRT_WALK_SPLIT");
+  const uint32_t H2 = G::WALK_SPLIT_HALF;
+  s->w_half = 16;
+  if (!hybrid && !s->w_general && (s->feature_mask & ~G::F_BASIC) == 0 && !(sp_env && strcmp(sp_env, "0") == 0) &&
+      (uint64_t)N * 16u <= H2 &&
+      total >= (uint64_t)H2 + 16u * N) {
+    uint32_t a = 0, q = 16u * N; /* node parts in pre-order, payloads in the gap, then behind the second half */
+    for (uint32_t i = 0; i < N; i++) {
+      addr[i] = a;
+      a += 16;
+    }
+    for (uint32_t i = 0; i < N; i++) {
+      if (T[i].leaf < 0) continue;
+      if (q + PB > H2 && q < H2 + 16u * N) q = H2 + 16u * N;
+      paddr[i] = q;
+      q += PB;
+    }
+    END = std::max(q, H2 + 16u * N);
+    s->w_half = H2;
+  }
   if (s->w_hot)
     for (uint32_t i = 0; i < N; i++)
       need(T[i].leaf < 0 || paddr[i] >= s->w_hot, HRT_ERR_STATE, "walk stream: a hybrid stream's payload in its staged part");
@@ -915,12 +937,12 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
     if (w.leaf < 0) {
       need(i + 1 < N, HRT_ERR_STATE, "walk stream: inner node without children");
       put4(o, addr[i], C[0], C[1], C[2], u2f(skip));
-      put4(o, addr[i] + 16, E[0], E[1], E[2], u2f(addr[i + 1])); /* pass: the first child */
+      put4(o, addr[i] + s->w_half, E[0], E[1], E[2], u2f(addr[i + 1])); /* pass: the first child */
       continue;
     }
     const WalkLeaf& L = leaves[w.leaf];
     put4(o, addr[i], C[0], C[1], C[2], u2f(skip));
-    put4(o, addr[i] + 16, E[0], E[1], E[2], u2f(paddr[i] | G::WALK_PEND));
+    put4(o, addr[i] + s->w_half, E[0], E[1], E[2], u2f(paddr[i] | G::WALK_PEND));
     if (s->w_general) { /* layout.h general-scene walk stream: the leaf's program range */
       const uint32_t q = paddr[i];
       uint32_t one = 0;
@@ -1886,6 +1908,7 @@ hrt_status hrt_debug_scene_blob(hrt_scene* s, void* out, uint64_t cap, uint64_t*
       info->walk_hot = s->w_hot;
       info->walk_general = s->w_general ? 1u : 0u;
       info->off_chains = s->off_chains;
+      info->walk_half = s->w_half;
     }
   });
 }

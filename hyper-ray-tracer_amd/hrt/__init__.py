@@ -107,7 +107,8 @@ class BlobInfo(ctypes.Structure):
          ("media_nested", ctypes.c_uint32), ("box_t0", ctypes.c_float), ("box_t1", ctypes.c_float),
          ("off_walk", ctypes.c_uint64), ("walk_bytes", ctypes.c_uint32), ("walk_regrouped", ctypes.c_uint32),
          ("bvh_tied_sorts", ctypes.c_uint32), ("walk_hot", ctypes.c_uint32),
-                ("walk_general", ctypes.c_uint32), ("off_chains", ctypes.c_uint64)]
+                ("walk_general", ctypes.c_uint32), ("off_chains", ctypes.c_uint64),
+        ("walk_half", ctypes.c_uint32)]
 
 
 class PresetInfo(ctypes.Structure):

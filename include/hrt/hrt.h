@@ -329,6 +329,8 @@ typedef struct hrt_blob_info {
   uint32_t walk_general;   /* 1: the walk stream is the general-scene stream (leaf programs, render_gwalk_kernel);
                             * 0: the sphere-scene stream (render_basic_kernel) */
   uint64_t off_chains;     /* every instance's transform chain, outermost first (layout.h CHAIN_F4) */
+  uint32_t walk_half;      /* bytes from a walk-stream node part's first 16 B to its second: 16, or the split of
+                            * sphere streams staged whole in LDS (layout.h WALK_SPLIT_HALF) */
 } hrt_blob_info;
 hrt_status hrt_debug_scene_blob(hrt_scene* s, void* out, uint64_t cap, uint64_t* size, hrt_blob_info* info);
 /* Overwrite n bytes of the committed scene's DEVICE blob at byte `offset` (hrt_blob_info offsets), after

@@ -61,6 +61,7 @@ void render_pixel(const KParams& P, uint32_t px, uint32_t py, float* rgba, uint6
           float closest = inf;
           WalkSrc src;
           src.base = P.walk;
+          src.half = P.walk_half;
           while (node < P.walk_end) {
             walk_box<true, WM_HOST>(src, node, r, P.t_min, closest, cn);
             if (walk_pending(node))
@@ -88,6 +89,7 @@ void render_pixel(const KParams& P, uint32_t px, uint32_t py, float* rgba, uint6
           if constexpr (CULL == G::CULL_EXACT) { /* the walk stream (layout.h), as the kernel walks it */
             WalkSrc src;
             src.base = P.walk;
+          src.half = P.walk_half;
             while (node < P.walk_end) walk_step_host<true>(P, src, node, r, closest, winner, cn);
           } else {
             while (node < P.main_end) basic_step<CULL, true>(P, P.nodes, P.prims, node, r, closest, winner, cn);
@@ -96,6 +98,7 @@ void render_pixel(const KParams& P, uint32_t px, uint32_t py, float* rgba, uint6
           if constexpr (CULL == G::CULL_EXACT) {
             WalkSrc src;
             src.base = P.walk;
+          src.half = P.walk_half;
             done = !traced || shade_walk<true, WM_HOST, true>(P, src, ps, winner, closest, r.o, r.d, r.time, r.tau, sum, cn) ||
                    ps.depth_left == 0;
           } else {
@@ -171,6 +174,7 @@ int lane_sim_render(const void* blob, const hrt_blob_info* bi, const hrt_camera*
   P.walk_bytes = bi->walk_bytes;
   P.walk_end = bi->walk_bytes;
   P.walk_hot = bi->walk_hot;
+  P.walk_half = bi->walk_half ? bi->walk_half : 16u;
   P.cam_origin = v3(cam->origin[0], cam->origin[1], cam->origin[2]);
   P.cam_llc = v3(cam->lower_left_corner[0], cam->lower_left_corner[1], cam->lower_left_corner[2]);
   P.cam_h = v3(cam->horizontal[0], cam->horizontal[1], cam->horizontal[2]);

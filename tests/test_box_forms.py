@@ -51,11 +51,12 @@ def _stream_boxes(name):
     raw = np.frombuffer(bytes(blob), np.uint8)
     base, end = int(info.off_walk), int(info.walk_bytes)
     boxes, o = [], 0
+    half = int(info.walk_half)  # a node part's second 16 B (layout.h WALK_SPLIT_HALF or 16)
     while o < end:  # pre-order over the node parts (tests/scenes.py general_stream_leaves)
-        c = raw[base + o:base + o + 32].view(np.float32)
-        u = raw[base + o:base + o + 32].view(np.uint32)
-        boxes.append(np.concatenate([c[:3], [0], c[4:7], [0]]))
-        o = int(u[3]) if u[7] & (1 << 31) else int(u[7])
+        a = raw[base + o:base + o + 16]
+        b = raw[base + o + half:base + o + half + 16]
+        boxes.append(np.concatenate([a.view(np.float32)[:3], [0], b.view(np.float32)[:3], [0]]))
+        o = int(a.view(np.uint32)[3]) if b.view(np.uint32)[3] & (1 << 31) else int(b.view(np.uint32)[3])
     return np.array(boxes, np.float32)
 
 

@@ -401,3 +401,19 @@ def test_nan_hit_path_is_all_nan(sim, earth):
         assert n == 50
         assert seg[3, 1] == 0.0 and seg[3, 4] == 0.0 and np.isnan(seg[3, 7])  # o.y = 0, d.y = 0, t = NaN
         assert np.isnan(seg[4:, 0]).all()
+
+
+@pytest.mark.parametrize("name", ["random"])
+def test_split_node_parts_equal_interleaved(sim, earth, name, monkeypatch):
+    """layout.h WALK_SPLIT_HALF: a sphere stream staged whole in LDS keeps each node part's second 16 B
+    16 KB after its first (all 16 bank slots of a ds_read_b128 lane group in use); bit for bit the walk over
+    32-B node parts (HRT_WALK_SPLIT=0), node for node. (Motion's 10.7-KB stream is too short to split: the second halves would not fit.)"""
+    _, info = hrt.scene_blob(hrt.preset(name, 1, earth))
+    assert info.walk_half == 16384 and info.walk_hot == 0
+    a, sa = sim_render(sim, name, 48, 27, 8, 50, 5, earth, kernel=0, cull=CULL_EXACT)
+    monkeypatch.setenv("HRT_WALK_SPLIT", "0")
+    _, info0 = hrt.scene_blob(hrt.preset(name, 1, earth))
+    assert info0.walk_half == 16
+    b, sb = sim_render(sim, name, 48, 27, 8, 50, 5, earth, kernel=0, cull=CULL_EXACT)
+    assert sa["segments"] == sb["segments"] and sa["nodes"] == sb["nodes"]
+    assert np.array_equal(a, b)
