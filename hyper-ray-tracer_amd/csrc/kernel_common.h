@@ -42,6 +42,7 @@ using namespace hrt::lane;
 struct PhaseClock {
   unsigned long long cyc[3];
   unsigned long long last;
+  unsigned long long leaf; /* inside cyc[1]: the batched leaf-test blocks (hrt_render_stats.leaf_cycles) */
 };
 
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {

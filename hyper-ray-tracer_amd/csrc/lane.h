@@ -282,8 +282,9 @@ template <int MEM>
 constexpr int payload_mem() { return MEM == WM_HYB ? WM_BUF : MEM; }
 
 #ifndef HRT_HYB_ANYG
-#define HRT_HYB_ANYG 1 /* skip the buffer loads of a step when every lane of the wave reads LDS (r04: C4 1/8 share
-                          * 5291 -> 5424 Mrays/s at 256 spp, A/B on one box; 0 for A/B) */
+#define HRT_HYB_ANYG 2 /* 2: the buffer loads under the exec mask of the lanes that need them (r04: C4 1/8 share at
+                          * 256 spp 5330 -> 5621 Mrays/s over 1, profiles/r04e_hyb_ab.txt); 1: skipped when no
+                          * lane of the wave needs them (5291 -> 5424 over 0); 0: every lane issues them */
 #endif
 /* Both 16-B halves of the node part at `off` (walk_box).  WM_HYB: every lane issues an LDS read AND a
  * buffer read of each half, into registers of their own, and keeps one by a select: the LDS lanes' buffer
@@ -295,7 +296,8 @@ HRT_LANE_FI void wload_node(const WalkSrc& src, uint32_t off, float4& a, float4&
 #if defined(__HIP_DEVICE_COMPILE__)
   if constexpr (MEM == WM_HYB) {
     const bool in_lds = off < src.hot;
-    const uint32_t loff = in_lds ? off : 0u, goff = in_lds ? 0x7FFFFF00u : off;
+    const uint32_t loff = in_lds ? off : 0u;
+    [[maybe_unused]] const uint32_t goff = in_lds ? 0x7FFFFF00u : off;
     const float4 la = wload<WM_LDS>(src, loff), lb = wload<WM_LDS>(src, loff + 16u);
 #if HRT_HYB_ANYG == 2
     /* the buffer loads only for the lanes that need them (exec mask), into registers of their own */
@@ -466,16 +468,22 @@ HRT_LANE_FI int sphere_pair_at(Vec3 c, float radius, Vec3 o, Vec3 d, float& t1, 
 }
 
 /* sphere.rs:38-55 / moving_sphere.rs:61-78: the accepted root only */
-HRT_LANE_FI bool sphere_root(const G::Prim* pp, uint32_t kind, const TRay& r, float tmin,
-                                            float tmax, float& root, bool motion_uniform) {
-  float4 p0 = ld4(pp->p0);
+/* the record's p0, p1 and p2[0] already in registers (gwalk_one) */
+HRT_LANE_FI bool sphere_root_v(const float4 p0, const float4 p1, float p2x, uint32_t kind, const TRay& r, float tmin,
+                               float tmax, float& root, bool motion_uniform) {
   Vec3 c = v3(p0.x, p0.y, p0.z);
   if (kind == G::P_MOVING) {
-    float4 p1 = ld4(pp->p1);
-    const float f = motion_uniform ? r.tau : (r.tau - p1.w) / pp->p2[0]; /* r.tau: the time (TRay) */
+    const float f = motion_uniform ? r.tau : (r.tau - p1.w) / p2x; /* r.tau: the time (TRay) */
     c = c + f * v3(p1.x, p1.y, p1.z);
   }
   return sphere_root_at(c, p0.w, r, tmin, tmax, root);
+}
+
+HRT_LANE_FI bool sphere_root(const G::Prim* pp, uint32_t kind, const TRay& r, float tmin,
+                                            float tmax, float& root, bool motion_uniform) {
+  const float4 p0 = ld4(pp->p0);
+  if (kind != G::P_MOVING) return sphere_root_v(p0, p0, 0.0f, kind, r, tmin, tmax, root, motion_uniform);
+  return sphere_root_v(p0, ld4(pp->p1), pp->p2[0], kind, r, tmin, tmax, root, motion_uniform);
 }
 
 /* Component i of v, and v with components a and b replaced, by selects: writing through Vec3's
@@ -496,13 +504,10 @@ HRT_LANE_FI void plane_axes(uint32_t plane, int& k, int& a, int& b) {
   else { k = 1; a = 2; b = 0; }
 }
 
-/* rect.rs:53-68 */
-HRT_LANE_FI bool rect_t(const G::Prim* pp, uint32_t plane, const TRay& r, float tmin,
-                                       float tmax, float& tout) {
+/* rect.rs:53-68 (p0 and k = p1[0] of the record) */
+HRT_LANE_FI bool rect_tv(const float4 p0, float kk, uint32_t plane, const TRay& r, float tmin, float tmax, float& tout) {
   int k, a, b;
   plane_axes(plane, k, a, b);
-  float4 p0 = ld4(pp->p0);
-  float kk = pp->p1[0];
   float t = (kk - comp(r.o, k)) / comp(r.d, k);
   if (t < tmin || t > tmax) return false;
   float av = comp(r.o, a) + t * comp(r.d, a);
@@ -510,6 +515,10 @@ HRT_LANE_FI bool rect_t(const G::Prim* pp, uint32_t plane, const TRay& r, float 
   if (av < p0.x || av > p0.y || bv < p0.z || bv > p0.w) return false;
   tout = t;
   return true;
+}
+
+HRT_LANE_FI bool rect_t(const G::Prim* pp, uint32_t plane, const TRay& r, float tmin, float tmax, float& tout) {
+  return rect_tv(ld4(pp->p0), pp->p1[0], plane, r, tmin, tmax, tout);
 }
 
 /* translation.rs:26-30 and rotation.rs:104-117: the ray handed to the child */
@@ -1449,42 +1458,75 @@ HRT_LANE_FI void walk_prim(const KParams& P, const WalkSrc& src, uint32_t& i, co
   walk_leaf_test<COUNT, MEM>(P, src, leaf, r, closest, winner, cn);
 }
 
-/* A one-node program (layout.h GL_ONE): trace_ray's body for a K_BOX_PRIM or K_PRIM node at i -- the
- * node's CULL_EXACT box test, then its rect or sphere against closest -- without the node loop and the
- * dispatch over every kind, whose code the wave otherwise runs for any lane that needs it. */
+/* A one-node program (layout.h GL_ONE): trace_ray's body for a K_BOX_PRIM or K_PRIM node -- the node's
+ * CULL_EXACT box test, then its rect or sphere against closest -- without the node loop and the dispatch over
+ * every kind, whose code the wave otherwise runs for any lane that needs it.  Everything is addressed from
+ * the payload (h.x the node, h.y its kind word, bmn.w the instance), so the node, its primitive and the
+ * instance chain are loaded together, before the group box test: ONE memory round trip after the payload's
+ * instead of up to three dependent ones (payload -> node -> primitive; payload -> chain -> its levels). */
 #ifndef HRT_GWALK_ONE
 #define HRT_GWALK_ONE 1
 #endif
-template <bool COUNT>
-HRT_LANE_FI void gwalk_one(const KParams& P, const G::Node* __restrict__ nodes, const G::Prim* __restrict__ prims,
-                           uint32_t i, const TRay& r, float tmin, float& closest, uint32_t& winner, Counts& cn) {
-  const G::Node* np = nodes + i;
-  const float4 a = ld4(np->mn);
-  const float4 b = ld4(np->mx);
-  const uint32_t kp = f2u(b.w);
-  if constexpr (COUNT) cn.nodes++;
-  if (((kp >> 24) & G::KIND_MASK) == G::K_BOX_PRIM &&
-      !box_hit<G::CULL_EXACT>(a, b, r, tmin, closest, (kp & G::NODE_REF_ONLY) != 0))
-    return;
-  const G::Prim* pp = prims + (kp & 0xFFFFFFu);
-  const uint32_t km = pp->km;
-  if constexpr (COUNT) cn.prims++;
-  float t;
-  bool h;
-  if ((km & 3u) == G::P_RECT) h = rect_t(pp, (km >> 2) & 3u, r, tmin, closest, t);
-  else h = sphere_root(pp, km & 3u, r, tmin, closest, t, P.motion_uniform != 0);
-  if (h) {
-    closest = t;
-    winner = i;
+HRT_LANE_FI void chain_turn(const float4 c0, const float4 c1, const float4 c2, const float4* ch, Vec3& o, Vec3& d) {
+  const uint32_t levels = f2u(c0.x); /* apply_chain_levels with the first two levels in registers */
+  if (levels > 0u) chain_level(c1, o, d);
+  if (levels > 1u) chain_level(c2, o, d);
+  for (uint32_t l = 2; l < levels; l++) chain_level(ch[1 + l], o, d);
+}
+
+HRT_LANE_FI void chain_derived(uint32_t flags, TRay& lr) {
+  /* 1/d and d.d of the turned direction where the program reads them (layout.h GL_INV / GL_DD) */
+  if (flags & G::GL_INV) {
+    lr.inv = v3(1.0f / lr.d.x, 1.0f / lr.d.y, 1.0f / lr.d.z);
+    set_noinv(lr); /* NaN mode in the innermost frame (box_hit in the program) */
+  }
+  if (flags & G::GL_DD) {
+    lr.dd = dot(lr.d, lr.d);
+    lr.rdd = div_rn_y(lr.dd);
   }
 }
 
-template <bool MEDIA, bool COUNT>
-HRT_LANE_FI void gwalk_program(const KParams& P, const G::Node* __restrict__ nodes, const G::Prim* __restrict__ prims,
-                               uint32_t flags, uint32_t begin, uint32_t end, const TRay& r, float& closest,
-                               uint32_t& winner, const PathKey& pk, Counts& cn) {
-  if (HRT_GWALK_ONE && (flags & G::GL_ONE)) gwalk_one<COUNT>(P, nodes, prims, begin, r, P.t_min, closest, winner, cn);
-  else trace_ray<G::CULL_EXACT, true, MEDIA, COUNT>(P, nodes, prims, begin, end, r, P.t_min, closest, winner, pk, cn);
+template <bool COUNT>
+HRT_LANE_FI void gwalk_one(const KParams& P, const G::Node* __restrict__ nodes, const G::Prim* __restrict__ prims,
+                           uint32_t flags, const float4 h, const float4 bmn, const float4 bmx, const TRay& r,
+                           float& closest, uint32_t& winner, uint32_t& gstate, Counts& cn) {
+  const uint32_t i = f2u(h.x), kp = f2u(h.y);
+  const G::Node* np = nodes + i;
+  const float4 a = ld4(np->mn), b = ld4(np->mx);
+  const G::Prim* pp = prims + (kp & 0xFFFFFFu);
+  const float4 p0 = ld4(pp->p0), p1 = ld4(pp->p1), p2 = ld4(pp->p2);
+  const bool inst = (flags & G::GL_INST) != 0u;
+  const float4* ch = P.chains + (size_t)(inst ? f2u(bmn.w) : 0u) * G::CHAIN_F4;
+  float4 c0 = p0, c1 = p0, c2 = p0;
+  if (inst) {
+    c0 = ch[0];
+    c1 = ch[1];
+    c2 = ch[2];
+  }
+  if (flags & G::GL_BOX) { /* the group's box: tested at the group's first leaf, the outcome kept (layout.h) */
+    const uint32_t g = f2u(bmx.w);
+    if ((gstate & 0x7FFFFFFFu) != g) gstate = g | (box_ref(bmn, bmx, r, P.t_min, closest) ? 0x80000000u : 0u);
+    if (!(gstate >> 31)) return;
+  }
+  TRay lr = r;
+  if (inst) {
+    chain_turn(c0, c1, c2, ch, lr.o, lr.d);
+    chain_derived(flags, lr);
+  }
+  if constexpr (COUNT) cn.nodes++;
+  if (((kp >> 24) & G::KIND_MASK) == G::K_BOX_PRIM &&
+      !box_hit<G::CULL_EXACT>(a, b, lr, P.t_min, closest, (kp & G::NODE_REF_ONLY) != 0))
+    return;
+  const uint32_t km = f2u(p2.w);
+  if constexpr (COUNT) cn.prims++;
+  float t;
+  bool hit;
+  if ((km & 3u) == G::P_RECT) hit = rect_tv(p0, p1.x, (km >> 2) & 3u, lr, P.t_min, closest, t);
+  else hit = sphere_root_v(p0, p1, p2.x, km & 3u, lr, P.t_min, closest, t, P.motion_uniform != 0);
+  if (hit) {
+    closest = t;
+    winner = i;
+  }
 }
 
 /* A passed leaf of the GENERAL walk stream (layout.h): the reference test of the enclosing BvhNode box
@@ -1496,34 +1538,27 @@ HRT_LANE_FI void gwalk_leaf_test(const KParams& P, const G::Node* __restrict__ n
                                  const WalkSrc& src, uint32_t leaf, const TRay& r, float& closest, uint32_t& winner,
                                  uint32_t& gstate, const PathKey& pk, Counts& cn) {
   constexpr int MEM = payload_mem<WMEM>();
-  const float4 h = wload<MEM>(src, leaf);
+  const float4 h = wload<MEM>(src, leaf), bmn = wload<MEM>(src, leaf + 16u), bmx = wload<MEM>(src, leaf + 32u);
   const uint32_t flags = f2u(h.z);
+  if (HRT_GWALK_ONE && (flags & G::GL_ONE)) {
+    gwalk_one<COUNT>(P, nodes, prims, flags, h, bmn, bmx, r, closest, winner, gstate, cn);
+    return;
+  }
   /* one call site for the program (the ray: the world ray, or the innermost instance frame's) */
   TRay lr = r;
-  if (flags & (G::GL_BOX | G::GL_INST)) {
-    const float4 bmn = wload<MEM>(src, leaf + 16u);
-    if (flags & G::GL_BOX) { /* the group's box: tested at the group's first leaf, the outcome kept (layout.h) */
-      const float4 bmx = wload<MEM>(src, leaf + 32u);
-      const uint32_t g = f2u(bmx.w);
-      if ((gstate & 0x7FFFFFFFu) != g) gstate = g | (box_ref(bmn, bmx, r, P.t_min, closest) ? 0x80000000u : 0u);
-      if (!(gstate >> 31)) return;
-    }
-    if (flags & G::GL_INST) {
-      /* a leaf of a flattened instance chain (layout.h GL_INST): the ray in the innermost instance's frame,
-       * as the reference's Translation / Rotation hits hand it down (apply_chain), with 1/d and d.d of the
-       * turned direction where the program reads them */
-      apply_chain(P, f2u(bmn.w), lr.o, lr.d);
-      if (flags & G::GL_INV) {
-        lr.inv = v3(1.0f / lr.d.x, 1.0f / lr.d.y, 1.0f / lr.d.z);
-        set_noinv(lr); /* NaN mode in the innermost frame (box_hit in the program) */
-      }
-      if (flags & G::GL_DD) {
-        lr.dd = dot(lr.d, lr.d);
-        lr.rdd = div_rn_y(lr.dd);
-      }
-    }
+  if (flags & G::GL_BOX) { /* as gwalk_one */
+    const uint32_t g = f2u(bmx.w);
+    if ((gstate & 0x7FFFFFFFu) != g) gstate = g | (box_ref(bmn, bmx, r, P.t_min, closest) ? 0x80000000u : 0u);
+    if (!(gstate >> 31)) return;
   }
-  gwalk_program<MEDIA, COUNT>(P, nodes, prims, flags, f2u(h.x), f2u(h.y), lr, closest, winner, pk, cn);
+  if (flags & G::GL_INST) {
+    /* a leaf of a flattened instance chain (layout.h GL_INST): the ray in the innermost instance's frame,
+     * as the reference's Translation / Rotation hits hand it down (apply_chain) */
+    apply_chain(P, f2u(bmn.w), lr.o, lr.d);
+    chain_derived(flags, lr);
+  }
+  const uint32_t begin = f2u(h.x), end = (flags & G::GL_ONE) ? begin + 1u : f2u(h.y); /* GL_ONE: h.y = kind word */
+  trace_ray<G::CULL_EXACT, true, MEDIA, COUNT>(P, nodes, prims, begin, end, lr, P.t_min, closest, winner, pk, cn);
 }
 
 template <bool MEDIA, bool COUNT, int MEM>

@@ -201,7 +201,9 @@ constexpr uint32_t WALK_NODE_BYTES = 32, WALK_PAYLOAD_BYTES = 96;
  * offset, its second 16 B (E, pass) WALK_SPLIT_HALF bytes further (an immediate offset of the LDS read),
  * so consecutive node parts lie 16 B apart in each half and a 16-lane group of ds_read_b128 spreads over
  * all 16 bank slots (interleaved 32-B parts use 8).  Node parts then occupy [0, 16 N) and
- * [WALK_SPLIT_HALF, WALK_SPLIT_HALF + 16 N); payloads fill the rest (N <= 1024). */
+ * [WALK_SPLIT_HALF, WALK_SPLIT_HALF + 16 N); payloads fill the rest (N <= 1024).  Opt-in (HRT_WALK_SPLIT=1):
+ * no faster on C2 (14 024 vs 14 038 Mrays/s, profiles/r04e_split_ab.txt), so the conflicts are not what
+ * bounds the step. */
 constexpr uint32_t WALK_SPLIT_HALF = 16384;
 constexpr uint32_t WL_MOVING = 1u, WL_NOBOX = 2u;
 enum : uint32_t { WT_SOLID = 0, WT_CHECKER = 1, WT_GLOBAL = 2 }; /* inline texture of a leaf's material */
@@ -215,7 +217,8 @@ enum : uint32_t { WT_SOLID = 0, WT_CHECKER = 1, WT_GLOBAL = 2 }; /* inline textu
  * member.  A leaf's PROGRAM is its range [begin, end) of the reference node stream, run by lane.h
  * trace_ray from the world ray (the leaf's own box node first: the reference test at the leaf).  Leaf
  * payload (GWALK_PAYLOAD_BYTES):
- *   float4(begin, end, flags, w)     w = successor << 2 (walk_successor, as in the sphere stream)
+ *   float4(begin, end, flags, w)     w = successor << 2 (walk_successor, as in the sphere stream); a GL_ONE
+ *                                         leaf holds the node's kind word in place of end (lane.h gwalk_one)
  *   float4(mn.xyz, inst) float4(mx.xyz, group)   GL_BOX: the nearest enclosing BvhNode box of a box-less
  *                                         leaf (world frame; `group` = that node's reference-stream index).
  *                                         The reference tests it once, before all the leaves it holds

@@ -315,7 +315,7 @@ hrt_status hguard(F&& f) {
   }
 }
 
-constexpr size_t SLOT_HDR = 128; /* work counter (8 B), stats words 0-11, error word 12, stats words 13-14 */
+constexpr size_t SLOT_HDR = 256; /* work counter (8 B), stats words 0-11, error word 12, stats words 13-15 */
 
 constexpr const char* SLOT_ERROR_MSG =
     "a render launch on this scene stopped walks that did not terminate (corrupt scene data); its frame is incomplete";
@@ -916,7 +916,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     /* the stats words and the watchdog's error word (h[12]) come back after EVERY launch, so a killed
      * frame is reported even when the caller asked for no stats (take_slot_error) */
     unsigned long long* h = (unsigned long long*)sl.h_tiles;
-    hip_check(hipMemcpyAsync(h, (uint8_t*)scratch + 8, 120, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(stats)");
+    hip_check(hipMemcpyAsync(h, (uint8_t*)scratch + 8, 128, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(stats)");
     hip_check(hipEventRecord((hipEvent_t)sl.event, stream), "hipEventRecord(slot)");
     sl.used = true;
     if (stats) {
@@ -934,6 +934,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
       for (int k = 0; k < 3; k++) stats->phase_cycles[k] = h[9 + k];
       stats->park_slots = h[13];
       stats->wait_slots = h[14];
+      stats->leaf_cycles = h[15];
     }
   });
 }

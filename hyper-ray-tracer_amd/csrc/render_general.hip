@@ -109,7 +109,7 @@ void render_gwalk_kernel(KParams P) {
   float closest = inf;
   uint32_t n_seg = 0, n_samples = 0, n_pixels = 0;
   Counts cn{0u, 0u, 0u, 0u, 0u, 0u};
-  PhaseClock pc{{0ull, 0ull, 0ull}, 0ull};
+  PhaseClock pc{{0ull, 0ull, 0ull}, 0ull, 0ull};
   auto stamp = [&](int phase) {
     if constexpr (COUNT) {
       const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -165,6 +165,7 @@ void render_gwalk_kernel(KParams P) {
         const bool waiting = pend != G::NONE && !(node < end);
         const unsigned long long pm = __ballot(waiting);
         if (pm && ((uint32_t)__popcll(pm) >= batch || !__ballot(node < end))) {
+          const unsigned long long t_leaf = COUNT ? __builtin_amdgcn_s_memtime() : 0ull;
           if constexpr (COUNT) cn.prim_slots++;
           if (pend != G::NONE) {
             const float before = closest;
@@ -183,6 +184,7 @@ void render_gwalk_kernel(KParams P) {
               node = walk_successor<WMEM>(ws, pend);
             }
           }
+          if constexpr (COUNT) pc.leaf += __builtin_amdgcn_s_memtime() - t_leaf;
         }
       }
       const unsigned long long live = __ballot(node < end || walk_pending(node) || pend != G::NONE);
@@ -244,6 +246,7 @@ void render_gwalk_kernel(KParams P) {
     flush_counts(P, cn);
     if (lane == 0)
       for (int k = 0; k < 3; k++) atomicAdd(&P.stats[9 + k], pc.cyc[k]);
+    if (lane == 0) atomicAdd(&P.stats[15], pc.leaf);
   }
 }
 

@@ -105,7 +105,7 @@ void render_basic_kernel(KParams P) {
   float closest = inf;
   uint32_t n_seg = 0, n_samples = 0, n_pixels = 0; /* wave totals (uniform) */
   Counts cn{0u, 0u, 0u, 0u, 0u, 0u};
-  PhaseClock pc{{0ull, 0ull, 0ull}, 0ull};
+  PhaseClock pc{{0ull, 0ull, 0ull}, 0ull, 0ull};
   auto stamp = [&](int phase) {
     if constexpr (COUNT) {
       const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -164,6 +164,7 @@ void render_basic_kernel(KParams P) {
           const bool waiting = pend != G::NONE && !(node < end);
           const unsigned long long pm = __ballot(waiting);
           if (pm && ((uint32_t)__popcll(pm) >= batch || !__ballot(node < end))) {
+            const unsigned long long t_leaf = COUNT ? __builtin_amdgcn_s_memtime() : 0ull;
             if constexpr (COUNT) cn.prim_slots++;
             if (pend != G::NONE) { /* the pending tests of every lane, walking or blocked, in walk order */
               walk_leaf_test<COUNT, WMEM>(P, ws, pend, r, closest, winner, cn);
@@ -173,6 +174,7 @@ void render_basic_kernel(KParams P) {
                 node = walk_successor<WMEM>(ws, pend);
               }
             }
+            if constexpr (COUNT) pc.leaf += __builtin_amdgcn_s_memtime() - t_leaf;
           }
           continue;
         }
@@ -244,6 +246,7 @@ void render_basic_kernel(KParams P) {
     flush_counts(P, cn);
     if (lane == 0)
       for (int k = 0; k < 3; k++) atomicAdd(&P.stats[9 + k], pc.cyc[k]);
+    if (lane == 0) atomicAdd(&P.stats[15], pc.leaf);
   }
 }
 

@@ -878,12 +878,12 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
     }
   need(off == total, HRT_ERR_STATE, "walk stream placement");
   uint32_t END = off;
-  /* split node parts (layout.h WALK_SPLIT_HALF): sphere streams staged whole in LDS that fill the space
-   * between the two halves with payloads (HRT_WALK_SPLIT=0 keeps 32-B parts) */
+  /* split node parts (layout.h WALK_SPLIT_HALF), opt-in (HRT_WALK_SPLIT=1): sphere streams staged whole in
+   * LDS that fill the space between the two halves with payloads */
   const char* sp_env = getenv("HRT_WALK_SPLIT");
   const uint32_t H2 = G::WALK_SPLIT_HALF;
   s->w_half = 16;
-  if (!hybrid && !s->w_general && (s->feature_mask & ~G::F_BASIC) == 0 && !(sp_env && strcmp(sp_env, "0") == 0) &&
+  if (!hybrid && !s->w_general && (s->feature_mask & ~G::F_BASIC) == 0 && sp_env && strcmp(sp_env, "1") == 0 &&
       (uint64_t)N * 16u <= H2 &&
       total >= (uint64_t)H2 + 16u * N) {
     uint32_t a = 0, q = 16u * N; /* node parts in pre-order, payloads in the gap, then behind the second half */
@@ -945,12 +945,15 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
     put4(o, addr[i] + s->w_half, E[0], E[1], E[2], u2f(paddr[i] | G::WALK_PEND));
     if (s->w_general) { /* layout.h general-scene walk stream: the leaf's program range */
       const uint32_t q = paddr[i];
-      uint32_t one = 0;
+      uint32_t one = 0, second = L.end; /* GL_ONE: the node's kind word instead of the range's end */
       if (L.end == L.begin + 1) {
         const uint32_t k = (s->g_nodes[L.begin].kp >> 24) & G::KIND_MASK;
-        if (k == G::K_BOX_PRIM || k == G::K_PRIM) one = G::GL_ONE;
+        if (k == G::K_BOX_PRIM || k == G::K_PRIM) {
+          one = G::GL_ONE;
+          second = s->g_nodes[L.begin].kp;
+        }
       }
-      put4(o, q, u2f(L.begin), u2f(L.end), u2f((L.has_rbox ? G::GL_BOX : 0u) | L.gflags | one), u2f(skip << 2));
+      put4(o, q, u2f(L.begin), u2f(second), u2f((L.has_rbox ? G::GL_BOX : 0u) | L.gflags | one), u2f(skip << 2));
       put4(o, q + 16, L.rbox.mn.x, L.rbox.mn.y, L.rbox.mn.z, u2f(L.inst));
       put4(o, q + 32, L.rbox.mx.x, L.rbox.mx.y, L.rbox.mx.z, u2f(L.rgroup));
       continue;

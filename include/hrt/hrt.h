@@ -112,13 +112,15 @@ typedef struct hrt_render_stats {
   uint64_t walk_slots;      /* HRT_RENDER_COUNT_WORK only: 64 x wave iterations of the node walk
                                (node_visits / walk_slots = SIMD lane utilisation of the walk) */
   uint64_t shade_slots;     /* HRT_RENDER_COUNT_WORK only: 64 x wave passes through shading */
-  uint64_t prim_slots;      /* HRT_RENDER_COUNT_WORK only: 64 x wave runs of the primitive block
-                               (sphere-scene kernel; 0 for the general kernel) */
-  uint64_t phase_cycles[3]; /* HRT_RENDER_COUNT_WORK, sphere-scene kernel: shader cycles summed over
+  uint64_t prim_slots;      /* HRT_RENDER_COUNT_WORK only: 64 x wave runs of the batched leaf-test block
+                               (walk kernels; 0 for the segment kernels) */
+  uint64_t phase_cycles[3]; /* HRT_RENDER_COUNT_WORK, walk kernels: shader cycles summed over
                                waves spent in [0] work claim + sample start, [1] walk, [2] shading */
-  uint64_t park_slots;      /* HRT_RENDER_COUNT_WORK, sphere-scene kernel: lane slots of walk steps spent parked on
+  uint64_t park_slots;      /* HRT_RENDER_COUNT_WORK, walk kernels: lane slots of walk steps spent parked on
                                a leaf (waiting for the batched primitive test) */
   uint64_t wait_slots;      /* ... spent with the walk done, waiting for the wave to leave the walk and shade */
+  uint64_t leaf_cycles;     /* HRT_RENDER_COUNT_WORK, walk kernels: the part of phase_cycles[1] spent in the batched
+                               leaf tests (sphere tests / leaf programs) */
 } hrt_render_stats;
 
 /* Scene description of one reference preset (application.rs:132-211). */

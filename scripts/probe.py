@@ -89,7 +89,8 @@ for key in flag_sets:
               f"shade-passes/ray {st.shade_slots/st.segments:.3f} prim-blocks/ray {st.prim_slots/st.segments:.2f} (x64 lanes)", flush=True)
         pcs = list(st.phase_cycles)
         if sum(pcs):
-            print("   phase cycles: claim+start {:.1%}  walk {:.1%}  shade {:.1%}".format(*[c / sum(pcs) for c in pcs]), flush=True)
+            print("   phase cycles: claim+start {:.1%}  walk {:.1%}  shade {:.1%}".format(*[c / sum(pcs) for c in pcs]),
+                  f" (leaf tests {st.leaf_cycles / sum(pcs):.1%} of all, inside walk)", flush=True)
         if st.walk_slots:
             ws = st.walk_slots
             print(f"   walk slots: stepping {st.node_visits/ws:.1%}  parked on a leaf {st.park_slots/ws:.1%}  "

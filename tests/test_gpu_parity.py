@@ -407,3 +407,15 @@ def test_hrt_render_tile_by_tile(earth):
     for x, y, w, h in hrt.tile_grid(W, H, 80):
         frame[y:y + h, x:x + w] = hrt.render(s, cam, p, region=(x, y, w, h))
     assert np.array_equal(frame, full)
+
+
+@pytest.mark.gpu
+def test_split_node_parts_render_the_same_frame(earth, monkeypatch):
+    """layout.h WALK_SPLIT_HALF (opt-in HRT_WALK_SPLIT=1): the sphere kernel's SPLIT instantiation reads each node
+    part's halves 16 KB apart; the frame and ray count equal the default 32-B parts' bit for bit."""
+    a, sa, s0 = _gpu_render("random", 160, 90, 16, 50, 3, earth)
+    assert hrt.scene_blob(s0)[1].walk_half == 16
+    monkeypatch.setenv("HRT_WALK_SPLIT", "1")
+    b, sb, s1 = _gpu_render("random", 160, 90, 16, 50, 3, earth)
+    assert hrt.scene_blob(s1)[1].walk_half == 16384
+    assert sa.segments == sb.segments and np.array_equal(a, b)

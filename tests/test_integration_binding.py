@@ -161,12 +161,12 @@ def test_struct_sizes_and_offsets_match_c(tmp_path):
         assert [f for f, *_ in py._fields_] == [f for f, _ in fields], ("python binding", name)
 
 
-def test_render_stats_is_112_bytes():
-    """The struct the round-2 binding had short by 16 bytes (park_slots / wait_slots)."""
+def test_render_stats_is_120_bytes():
+    """The struct the round-2 binding had short by 16 bytes (park_slots / wait_slots); r04 added leaf_cycles."""
     ds, _, _ = doc_api()
     names = [f for f, _ in ds["hrt_render_stats"]]
-    assert names[-2:] == ["park_slots", "wait_slots"]
-    assert ctypes.sizeof(hrt.RenderStats) == 112
+    assert names[-3:] == ["park_slots", "wait_slots", "leaf_cycles"]
+    assert ctypes.sizeof(hrt.RenderStats) == 120
 
 
 @pytest.mark.parametrize("name", ["hrt_scene_synchronize", "hrt_scene_get_info", "hrt_render_device", "hrt_preset_build"])

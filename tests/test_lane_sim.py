@@ -407,7 +407,8 @@ def test_nan_hit_path_is_all_nan(sim, earth):
 def test_split_node_parts_equal_interleaved(sim, earth, name, monkeypatch):
     """layout.h WALK_SPLIT_HALF: a sphere stream staged whole in LDS keeps each node part's second 16 B
     16 KB after its first (all 16 bank slots of a ds_read_b128 lane group in use); bit for bit the walk over
-    32-B node parts (HRT_WALK_SPLIT=0), node for node. (Motion's 10.7-KB stream is too short to split: the second halves would not fit.)"""
+    32-B node parts (the default), node for node (opt-in: HRT_WALK_SPLIT=1)."""
+    monkeypatch.setenv("HRT_WALK_SPLIT", "1")
     _, info = hrt.scene_blob(hrt.preset(name, 1, earth))
     assert info.walk_half == 16384 and info.walk_hot == 0
     a, sa = sim_render(sim, name, 48, 27, 8, 50, 5, earth, kernel=0, cull=CULL_EXACT)
