@@ -609,6 +609,38 @@ struct PathKey {
 #ifndef HRT_MEDIUM_PAIR
 #define HRT_MEDIUM_PAIR 1 /* 0: a one-sphere medium boundary takes the two boundary walks (A/B) */
 #endif
+
+/* A medium's boundary that is ONE sphere / moving sphere (Medium.sphere; its record p0, p1, p2 in registers):
+ * both boundary queries of constant_medium.rs:37-48 from one evaluation of the quadratic (sphere_pair_at),
+ * the sphere at the ray's time as moving_sphere.rs:55-58 computes it.  Returns the number of hits. */
+HRT_LANE_FI int medium_pair(const KParams& P, const float4 p0, const float4 p1, float p2x, uint32_t km, const TRay& r,
+                            float& c1, float& c2) {
+  Vec3 c = v3(p0.x, p0.y, p0.z);
+  if ((km & 3u) == G::P_MOVING) {
+    const float tau = P.motion_uniform ? (r.time - P.motion_t0) / P.motion_span : r.time;
+    const float f = P.motion_uniform ? tau : (tau - p1.w) / p2x;
+    c = c + f * v3(p1.x, p1.y, p1.z);
+  }
+  return sphere_pair_at(c, p0.w, r.o, r.d, c1, c2);
+}
+
+/* constant_medium.rs:50-76 after the two boundary hits c1 < c2: the scatter distance against the part of
+ * [c1, c2] in [tmin, closest]; a scatter becomes the closest hit, at the medium node `here` */
+HRT_LANE_FI void medium_scatter(const KParams& P, const G::Medium& m, float c1, float c2, const TRay& r, float tmin,
+                                float& closest, uint32_t& winner, uint32_t here, const PathKey& pk) {
+  float r1 = c1, r2 = c2;
+  if (r1 < tmin) r1 = tmin;
+  if (r2 > closest) r2 = closest;
+  if (r1 >= r2) return;
+  if (r1 < 0.0f) r1 = 0.0f;
+  const float ray_length = sqrtf(r.dd);
+  const float inside = (r2 - r1) * ray_length;
+  const float xi = medium_xi(pk.pkey, pk.segment, m.medium_id);
+  const float hit_distance = m.neg_inv_density * (ln_f(xi) / P.ln_e);
+  if (hit_distance > inside) return;
+  closest = r1 + hit_distance / ray_length;
+  winner = here;
+}
 /* The world walk.  Closest hit over [begin, end) of the node stream with t in [tmin, closest]:
  * `winner` = node index of the accepted leaf (NONE if nothing).  MEDIA: ConstantMedium nodes are
  * evaluated (their boundary walks are nested calls with MEDIA = false). */
@@ -695,15 +727,7 @@ HRT_LANE void trace_ray(const KParams& P, const G::Node* __restrict__ nodes, con
             float c1 = inf, c2 = inf;
             if (HRT_MEDIUM_PAIR && m.sphere != G::NONE) { /* one sphere: both queries from one quadratic */
               const G::Prim* bp = prims + m.sphere;
-              const float4 p0 = ld4(bp->p0);
-              Vec3 c = v3(p0.x, p0.y, p0.z);
-              if ((bp->km & 3u) == G::P_MOVING) { /* moving_sphere.rs:55-58 at the ray's time (set_time) */
-                const float4 p1 = ld4(bp->p1);
-                const float tau = P.motion_uniform ? (r.time - P.motion_t0) / P.motion_span : r.time;
-                const float f = P.motion_uniform ? tau : (tau - p1.w) / bp->p2[0];
-                c = c + f * v3(p1.x, p1.y, p1.z);
-              }
-              const int hits = sphere_pair_at(c, p0.w, r.o, r.d, c1, c2);
+              const int hits = medium_pair(P, ld4(bp->p0), ld4(bp->p1), bp->p2[0], bp->km, r, c1, c2);
               if constexpr (COUNT) { /* the work counters of the two boundary walks it replaces */
                 cn.nodes += hits > 0 ? 2u : 1u;
                 cn.prims += hits > 0 ? 2u : 1u;
@@ -716,18 +740,7 @@ HRT_LANE void trace_ray(const KParams& P, const G::Node* __restrict__ nodes, con
               trace<CULL, FULL, false, COUNT>(P, nodes, prims, m.bstart, m.bend, r.o, r.d, r.time, c1 + 0.0001f, c2, w2, pk, cn);
               if (w2 == G::NONE) continue;
             }
-            float r1 = c1, r2 = c2;
-            if (r1 < tmin) r1 = tmin;
-            if (r2 > closest) r2 = closest;
-            if (r1 >= r2) continue;
-            if (r1 < 0.0f) r1 = 0.0f;
-            float ray_length = sqrtf(r.dd);
-            float inside = (r2 - r1) * ray_length;
-            float xi = medium_xi(pk.pkey, pk.segment, m.medium_id);
-            float hit_distance = m.neg_inv_density * (ln_f(xi) / P.ln_e);
-            if (hit_distance > inside) continue;
-            closest = r1 + hit_distance / ray_length;
-            winner = here;
+            medium_scatter(P, m, c1, c2, r, tmin, closest, winner, here, pk);
           }
         }
       }
@@ -1533,6 +1546,37 @@ HRT_LANE_FI void gwalk_one(const KParams& P, const G::Node* __restrict__ nodes, 
  * (box-less leaves, GL_BOX), then the leaf's program -- its range of the reference stream, whose first
  * node is the leaf's own box (the reference test at the leaf) -- from the world ray
  * against the lane's current closest.  The winner is a reference-stream node index (make_record<true>). */
+/* A medium leaf over one sphere (layout.h GL_MED): trace_ray over its program [the ConstantMedium's box node,
+ * its K_MEDIUM node] without the node loop, the box node, the medium record and the boundary sphere loaded
+ * together (h.x the box node, h.y the medium, bmn.w the sphere) */
+template <bool COUNT>
+HRT_LANE_FI void gwalk_medium(const KParams& P, const G::Node* __restrict__ nodes, const G::Prim* __restrict__ prims,
+                              uint32_t flags, const float4 h, const float4 bmn, const float4 bmx, const TRay& r,
+                              float& closest, uint32_t& winner, uint32_t& gstate, const PathKey& pk, Counts& cn) {
+  const uint32_t i = f2u(h.x);
+  const G::Node* np = nodes + i;
+  const float4 a = ld4(np->mn), b = ld4(np->mx);
+  const G::Medium m = P.media[f2u(h.y)];
+  const G::Prim* bp = prims + f2u(bmn.w);
+  const float4 p0 = ld4(bp->p0), p1 = ld4(bp->p1), p2 = ld4(bp->p2);
+  if (flags & G::GL_BOX) { /* as gwalk_one */
+    const uint32_t g = f2u(bmx.w);
+    if ((gstate & 0x7FFFFFFFu) != g) gstate = g | (box_ref(bmn, bmx, r, P.t_min, closest) ? 0x80000000u : 0u);
+    if (!(gstate >> 31)) return;
+  }
+  if constexpr (COUNT) cn.nodes++;
+  if (!box_hit<G::CULL_EXACT>(a, b, r, P.t_min, closest, (f2u(b.w) & G::NODE_REF_ONLY) != 0)) return;
+  if constexpr (COUNT) cn.nodes++; /* the K_MEDIUM node */
+  float c1 = u2f(0x7f800000u), c2 = c1;
+  const int hits = medium_pair(P, p0, p1, p2.x, f2u(p2.w), r, c1, c2);
+  if constexpr (COUNT) { /* the work counters of the two boundary walks it replaces (trace_ray) */
+    cn.nodes += hits > 0 ? 2u : 1u;
+    cn.prims += hits > 0 ? 2u : 1u;
+  }
+  if (hits < 2) return;
+  medium_scatter(P, m, c1, c2, r, P.t_min, closest, winner, i + 1u, pk);
+}
+
 template <bool MEDIA, bool COUNT, int WMEM>
 HRT_LANE_FI void gwalk_leaf_test(const KParams& P, const G::Node* __restrict__ nodes, const G::Prim* __restrict__ prims,
                                  const WalkSrc& src, uint32_t leaf, const TRay& r, float& closest, uint32_t& winner,
@@ -1544,6 +1588,12 @@ HRT_LANE_FI void gwalk_leaf_test(const KParams& P, const G::Node* __restrict__ n
     gwalk_one<COUNT>(P, nodes, prims, flags, h, bmn, bmx, r, closest, winner, gstate, cn);
     return;
   }
+  if constexpr (MEDIA) {
+    if (HRT_GWALK_ONE && (flags & G::GL_MED)) {
+      gwalk_medium<COUNT>(P, nodes, prims, flags, h, bmn, bmx, r, closest, winner, gstate, pk, cn);
+      return;
+    }
+  }
   /* one call site for the program (the ray: the world ray, or the innermost instance frame's) */
   TRay lr = r;
   if (flags & G::GL_BOX) { /* as gwalk_one */
@@ -1551,13 +1601,14 @@ HRT_LANE_FI void gwalk_leaf_test(const KParams& P, const G::Node* __restrict__ n
     if ((gstate & 0x7FFFFFFFu) != g) gstate = g | (box_ref(bmn, bmx, r, P.t_min, closest) ? 0x80000000u : 0u);
     if (!(gstate >> 31)) return;
   }
-  if (flags & G::GL_INST) {
+  if (flags & G::GL_INST) { /* (never with GL_MED: bmn.w is then the boundary sphere) */
     /* a leaf of a flattened instance chain (layout.h GL_INST): the ray in the innermost instance's frame,
      * as the reference's Translation / Rotation hits hand it down (apply_chain) */
     apply_chain(P, f2u(bmn.w), lr.o, lr.d);
     chain_derived(flags, lr);
   }
-  const uint32_t begin = f2u(h.x), end = (flags & G::GL_ONE) ? begin + 1u : f2u(h.y); /* GL_ONE: h.y = kind word */
+  const uint32_t begin = f2u(h.x); /* GL_ONE: h.y = the node's kind word; GL_MED: the medium (layout.h) */
+  const uint32_t end = (flags & G::GL_ONE) ? begin + 1u : (flags & G::GL_MED) ? begin + 2u : f2u(h.y);
   trace_ray<G::CULL_EXACT, true, MEDIA, COUNT>(P, nodes, prims, begin, end, lr, P.t_min, closest, winner, pk, cn);
 }
 

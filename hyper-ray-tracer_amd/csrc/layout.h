@@ -196,6 +196,11 @@ constexpr uint32_t WALK_PEND = 1u << 31;
  * each also holding a u32 result slot for each of its (at most 768) threads */
 constexpr uint32_t LDS_SCENE_MAX_BYTES = 77u * 1024u;
 static_assert(2u * (LDS_SCENE_MAX_BYTES + 768u * 4u) <= 160u * 1024u, "two sphere workgroups per CU");
+/* a GENERAL walk stream beyond LDS_SCENE_MAX_BYTES stages this much of its node parts: the general kernel then
+ * runs one 1024-thread workgroup per CU (16 waves, the 4 waves/SIMD of two 512-thread ones; render_general.hip
+ * BIG) with the node parts a ray is likeliest to reach in LDS, twice the two-workgroup budget */
+constexpr uint32_t GWALK_LDS_BIG_BYTES = 152u * 1024u;
+static_assert(GWALK_LDS_BIG_BYTES + 1024u * 4u <= 160u * 1024u, "one 1024-thread general workgroup per CU");
 constexpr uint32_t WALK_NODE_BYTES = 32, WALK_PAYLOAD_BYTES = 96;
 /* Split node parts (r04, sphere streams staged whole in LDS): a node part's first 16 B (C, skip) at its
  * offset, its second 16 B (E, pass) WALK_SPLIT_HALF bytes further (an immediate offset of the LDS read),
@@ -218,7 +223,8 @@ enum : uint32_t { WT_SOLID = 0, WT_CHECKER = 1, WT_GLOBAL = 2 }; /* inline textu
  * trace_ray from the world ray (the leaf's own box node first: the reference test at the leaf).  Leaf
  * payload (GWALK_PAYLOAD_BYTES):
  *   float4(begin, end, flags, w)     w = successor << 2 (walk_successor, as in the sphere stream); a GL_ONE
- *                                         leaf holds the node's kind word in place of end (lane.h gwalk_one)
+ *                                         leaf holds the node's kind word in place of end (lane.h gwalk_one),
+ *                                         a GL_MED leaf its medium
  *   float4(mn.xyz, inst) float4(mx.xyz, group)   GL_BOX: the nearest enclosing BvhNode box of a box-less
  *                                         leaf (world frame; `group` = that node's reference-stream index).
  *                                         The reference tests it once, before all the leaves it holds
@@ -241,6 +247,10 @@ constexpr uint32_t GL_BOX = 1u, GL_INST = 2u, GL_DIR = 4u, GL_INV = 8u, GL_DD = 
 /* GL_ONE: the program is ONE primitive node (K_BOX_PRIM or K_PRIM: a BvhNode leaf, a Cuboid side, a List
  * member), run without trace_ray's node loop and kind dispatch (lane.h gwalk_one) */
 constexpr uint32_t GL_ONE = 32u;
+/* GL_MED: the program is [a ConstantMedium's box node, its K_MEDIUM node] at world level with a one-sphere
+ * boundary (Medium.sphere); the payload holds the medium in place of end and the sphere in place of the
+ * instance (lane.h gwalk_medium) */
+constexpr uint32_t GL_MED = 64u;
 
 }  // namespace gpu
 }  // namespace hrt

@@ -454,7 +454,9 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
                        s->g_mats.size() * sizeof(G::Mat) + s->g_texs.size() * sizeof(G::Tex) +
                        s->g_chains.size() * sizeof(float);
     const bool no_lds = (flags & HRT_RENDER_NO_LDS) != 0;
-    pl.gwalk_mem = no_lds || walk > LDS_SCENE_MAX ? WM_BUF : (s->w_hot ? WM_HYB : WM_LDS);
+    /* a hybrid general stream's staged part may take one 1024-thread workgroup's LDS (GWALK_LDS_BIG_BYTES) */
+    pl.gwalk_mem = no_lds || walk > (s->w_hot ? (size_t)G::GWALK_LDS_BIG_BYTES : LDS_SCENE_MAX) ? WM_BUF
+                                                                                             : (s->w_hot ? WM_HYB : WM_LDS);
     const char* lr = getenv("HRT_GWALK_LREF"); /* A/B knob: "0" keeps the reference stream in global memory */
     pl.gwalk_lref = pl.gwalk_mem == WM_LDS && walk + ref <= LDS_SCENE_MAX && !(lr && strcmp(lr, "0") == 0);
     pl.smem = pl.gwalk_mem == WM_BUF ? 0 : walk + (pl.gwalk_lref ? ref : 0);

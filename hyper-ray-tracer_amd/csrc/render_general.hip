@@ -33,8 +33,9 @@ constexpr int GWALK_WAVES = HRT_GWALK_WAVES;
 /* WMEM: where the walk stream is read (WM_LDS: staged whole; WM_HYB: its top levels staged, the rest
  * through the buffer descriptor; WM_BUF: global memory).  LREF: the reference node stream and the
  * primitives that leaf programs read are staged in LDS behind the walk stream. */
-template <bool COUNT, int WMEM, bool LREF, int TRIM>
-__global__ __launch_bounds__(128 * GWALK_WAVES, GWALK_WAVES)
+/* BIG: one 1024-thread workgroup per CU (a hybrid stream's staged part beyond LDS_SCENE_MAX_BYTES) */
+template <bool COUNT, int WMEM, bool LREF, int TRIM, bool BIG>
+__global__ __launch_bounds__((BIG ? 256 : 128) * GWALK_WAVES, GWALK_WAVES)
 void render_gwalk_kernel(KParams P) {
   extern __shared__ float4 lds_scene[];
   constexpr bool MEDIA = !(TRIM & TRIM_MEDIA);
@@ -250,15 +251,15 @@ void render_gwalk_kernel(KParams P) {
   }
 }
 
-template <bool COUNT, int WMEM, bool LREF, int TRIM>
+template <bool COUNT, int WMEM, bool LREF, int TRIM, bool BIG = false>
 void launch_g(const KParams& kp, int device, hipStream_t stream, size_t smem) {
-  const void* fn = (const void*)render_gwalk_kernel<COUNT, WMEM, LREF, TRIM>;
-  const int block = 128 * GWALK_WAVES;
+  const void* fn = (const void*)render_gwalk_kernel<COUNT, WMEM, LREF, TRIM, BIG>;
+  const int block = (BIG ? 256 : 128) * GWALK_WAVES;
   KParams p = kp;
   p.lane_lds = (uint32_t)((smem + 15) & ~(size_t)15);
   const size_t total = p.lane_lds + (size_t)block * sizeof(uint32_t);
   const int grid = resident_grid(fn, block, device, total, true, __PRETTY_FUNCTION__);
-  hipLaunchKernelGGL((render_gwalk_kernel<COUNT, WMEM, LREF, TRIM>), dim3(grid), dim3(block), total, stream, p);
+  hipLaunchKernelGGL((render_gwalk_kernel<COUNT, WMEM, LREF, TRIM, BIG>), dim3(grid), dim3(block), total, stream, p);
   hip_check(hipGetLastError(), "render_gwalk_kernel launch");
 }
 
@@ -266,6 +267,7 @@ template <bool COUNT, int TRIM>
 void launch_g_mem(int wmem, bool lref, const KParams& kp, int device, hipStream_t stream, size_t smem) {
   if (wmem == WM_LDS) lref ? launch_g<COUNT, WM_LDS, true, TRIM>(kp, device, stream, smem)
                            : launch_g<COUNT, WM_LDS, false, TRIM>(kp, device, stream, smem);
+  else if (wmem == WM_HYB && smem > G::LDS_SCENE_MAX_BYTES) launch_g<COUNT, WM_HYB, false, TRIM, true>(kp, device, stream, smem);
   else if (wmem == WM_HYB) launch_g<COUNT, WM_HYB, false, TRIM>(kp, device, stream, smem);
   else launch_g<COUNT, WM_BUF, false, TRIM>(kp, device, stream, smem);
 }

@@ -816,6 +816,11 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
   need(total < (1ull << 30), HRT_ERR_UNSUPPORTED, "scene too large for the walk stream");
   std::vector<uint32_t> addr(N), paddr(N, 0);
   const char* hot_env = getenv("HRT_WALK_HOT"); /* "0": no LDS-staged top levels (A/B) */
+  /* the staged budget: general streams twice the sphere kernel's (layout.h GWALK_LDS_BIG_BYTES; HRT_GWALK_BIG=0
+   * keeps LDS_SCENE_MAX_BYTES, A/B) */
+  const char* big_env = getenv("HRT_GWALK_BIG");
+  const uint32_t budget = s->w_general && !(big_env && strcmp(big_env, "0") == 0) ? G::GWALK_LDS_BIG_BYTES
+                                                                                   : G::LDS_SCENE_MAX_BYTES;
   const bool hybrid = total > G::LDS_SCENE_MAX_BYTES && !(hot_env && strcmp(hot_env, "0") == 0);
   uint32_t off = 0;
   std::vector<char> hot(N, 0);
@@ -846,7 +851,7 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
       std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return T[a].depth < T[b].depth; });
     }
     for (uint32_t i : order) {
-      if (off + G::WALK_NODE_BYTES > G::LDS_SCENE_MAX_BYTES) break;
+      if (off + G::WALK_NODE_BYTES > budget) break;
       addr[i] = off;
       off += G::WALK_NODE_BYTES;
       hot[i] = 1;
@@ -945,16 +950,28 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
     put4(o, addr[i] + s->w_half, E[0], E[1], E[2], u2f(paddr[i] | G::WALK_PEND));
     if (s->w_general) { /* layout.h general-scene walk stream: the leaf's program range */
       const uint32_t q = paddr[i];
-      uint32_t one = 0, second = L.end; /* GL_ONE: the node's kind word instead of the range's end */
+      /* GL_ONE: the node's kind word instead of the range's end; GL_MED: the medium, and the boundary
+       * sphere instead of the (world-level) instance */
+      uint32_t one = 0, second = L.end, fourth = L.inst;
       if (L.end == L.begin + 1) {
         const uint32_t k = (s->g_nodes[L.begin].kp >> 24) & G::KIND_MASK;
         if (k == G::K_BOX_PRIM || k == G::K_PRIM) {
           one = G::GL_ONE;
           second = s->g_nodes[L.begin].kp;
         }
+      } else if (L.end == L.begin + 2 && !(L.gflags & G::GL_INST) && L.inst == G::NONE) {
+        const uint32_t k0 = (s->g_nodes[L.begin].kp >> 24) & G::KIND_MASK;
+        const uint32_t k1 = (s->g_nodes[L.begin + 1].kp >> 24) & G::KIND_MASK;
+        const uint32_t mi = s->g_nodes[L.begin + 1].kp & 0xFFFFFFu;
+        const char* me = getenv("HRT_GWALK_MED"); /* "0": media leaves run trace_ray (A/B) */
+        if (k0 == G::K_BOX && k1 == G::K_MEDIUM && s->g_media[mi].sphere != G::NONE && !(me && strcmp(me, "0") == 0)) {
+          one = G::GL_MED;
+          second = mi;
+          fourth = s->g_media[mi].sphere;
+        }
       }
       put4(o, q, u2f(L.begin), u2f(second), u2f((L.has_rbox ? G::GL_BOX : 0u) | L.gflags | one), u2f(skip << 2));
-      put4(o, q + 16, L.rbox.mn.x, L.rbox.mn.y, L.rbox.mn.z, u2f(L.inst));
+      put4(o, q + 16, L.rbox.mn.x, L.rbox.mn.y, L.rbox.mn.z, u2f(fourth));
       put4(o, q + 32, L.rbox.mx.x, L.rbox.mx.y, L.rbox.mx.z, u2f(L.rgroup));
       continue;
     }

@@ -17,6 +17,7 @@ import hrt
 PEND = 1 << 31
 GL_BOX = 1
 GL_ONE = 32
+GL_MED = 64
 
 
 def perlin_tables(seed):
@@ -97,7 +98,7 @@ def camera(w, h):
 
 def general_stream_leaves(blob, info):
     """The general walk stream's leaves in walk (pre-)order: (begin, end, flags, group) per leaf (a GL_ONE leaf
-    keeps its node's kind word in place of end: layout.h)."""
+    keeps its node's kind word in place of end, a GL_MED leaf its medium: layout.h)."""
     raw = np.frombuffer(bytes(blob), np.uint8)
     base = int(info.off_walk)
     end = int(info.walk_bytes)
@@ -109,8 +110,9 @@ def general_stream_leaves(blob, info):
         if link & PEND:
             p = link & ~PEND
             h, bmx = u32(p), u32(p + 32)
-            one = int(h[2]) & GL_ONE
-            out.append((int(h[0]), int(h[0]) + 1 if one else int(h[1]), int(h[2]), int(bmx[3])))
+            fl = int(h[2])
+            last = int(h[0]) + 1 if fl & GL_ONE else int(h[0]) + 2 if fl & GL_MED else int(h[1])
+            out.append((int(h[0]), last, fl, int(bmx[3])))
             o = skip
         else:
             o = link
