@@ -39,6 +39,18 @@ using namespace hrt::lane;
 
 /* COUNT builds of the sphere-scene kernel: shader-clock cycles per wave phase (s_memtime stamps,
  * uniform per wave): [0] claim + sample start, [1] walk, [2] shading */
+/* The walk kernels recompute the ray's derived fields (1/d, the inflated test's origin term, d.d, RN(1/d.d):
+ * lane.h set_dir) for EVERY lane at the top of every pass, the same bits again for a lane in mid-walk: they
+ * are then dead across the shading code, which otherwise keeps them in registers (or scratch) for the lanes
+ * still walking.  The wave runs set_dir's instructions each pass for its new rays anyway.  0: only new rays
+ * (A/B; profiles/r04g_rederive_ab.txt). */
+#ifndef HRT_RAY_REDERIVE
+#define HRT_RAY_REDERIVE 1 /* the general kernel (r04: Cornell-smoke +4.9%, Final neutral, bit-identical) */
+#endif
+#ifndef HRT_RAY_REDERIVE_SPHERE
+#define HRT_RAY_REDERIVE_SPHERE 0 /* the sphere kernel (r04: C2 -3%, C3 -0.7%: its shading spills nothing) */
+#endif
+
 struct PhaseClock {
   unsigned long long cyc[3];
   unsigned long long last;

@@ -1145,11 +1145,16 @@ HRT_LANE_FI bool scatter(PathState& ps, const Rec& rec, uint32_t kind, Vec3 albe
   return false;
 }
 
-enum : int { TRIM_MEDIA = 1, TRIM_HEAVY_TEX = 2 };
+/* TRIM_PROGRAMS (general walk kernel): every leaf program is a one-node or one-sphere-medium one (layout.h
+ * GL_ONE / GL_MED; scene w_generic false), so trace_ray's generic program is not compiled in */
+enum : int { TRIM_MEDIA = 1, TRIM_HEAVY_TEX = 2, TRIM_PROGRAMS = 4 };
 
 /* The part of one ray_color step after world.hit (application.rs:483-494): background on a miss,
  * else hit record, emission and scatter.  (ro, rd, rtime) is the segment just traced; the scattered
  * ray goes to ps.ro/ps.rd.  Returns true when the path is finished. */
+#ifndef HRT_GEN_TEX_INLINE
+#define HRT_GEN_TEX_INLINE 0 /* 1: the segment / general kernels evaluate the noise texture inline (A/B) */
+#endif
 template <bool FULL, bool COUNT, int TRIM = 0>
 HRT_LANE_FI bool shade(const KParams& P, PathState& ps, uint32_t winner, float closest, Vec3 ro,
                                       Vec3 rd, float rtime, float tau, Counts& cn) {
@@ -1160,7 +1165,7 @@ HRT_LANE_FI bool shade(const KParams& P, PathState& ps, uint32_t winner, float c
   const Rec rec = make_record<FULL>(P, winner, closest, ro, rd, rtime, tau);
   const G::Mat M = P.mats[rec.mat];
   return scatter<FULL>(ps, rec, M.kind, v3(M.a[0], M.a[1], M.a[2]), M.a[3], M.a[0], rd,
-                       [&]() { return tex_value<FULL && !(TRIM & TRIM_HEAVY_TEX), COUNT>(P, M.tex, rec.u, rec.v, rec.p, cn); });
+                       [&]() { return tex_value<FULL && !(TRIM & TRIM_HEAVY_TEX), COUNT, HRT_GEN_TEX_INLINE != 0>(P, M.tex, rec.u, rec.v, rec.p, cn); });
 }
 
 /* shade() for the sphere kernel's walk stream: the winner is a leaf record (layout.h), which holds the
@@ -1577,7 +1582,7 @@ HRT_LANE_FI void gwalk_medium(const KParams& P, const G::Node* __restrict__ node
   medium_scatter(P, m, c1, c2, r, P.t_min, closest, winner, i + 1u, pk);
 }
 
-template <bool MEDIA, bool COUNT, int WMEM>
+template <bool MEDIA, bool COUNT, int WMEM, bool PROG = true>
 HRT_LANE_FI void gwalk_leaf_test(const KParams& P, const G::Node* __restrict__ nodes, const G::Prim* __restrict__ prims,
                                  const WalkSrc& src, uint32_t leaf, const TRay& r, float& closest, uint32_t& winner,
                                  uint32_t& gstate, const PathKey& pk, Counts& cn) {
@@ -1594,6 +1599,7 @@ HRT_LANE_FI void gwalk_leaf_test(const KParams& P, const G::Node* __restrict__ n
       return;
     }
   }
+  if constexpr (!PROG) return; /* (no such leaf: TRIM_PROGRAMS) */
   /* one call site for the program (the ray: the world ray, or the innermost instance frame's) */
   TRay lr = r;
   if (flags & G::GL_BOX) { /* as gwalk_one */

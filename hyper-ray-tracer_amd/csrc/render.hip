@@ -467,6 +467,8 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
     pl.lds = pl.gwalk_mem != WM_BUF;
     pl.trim = ((s->feature_mask & (G::F_NOISE | G::F_IMAGE)) == 0 ? TRIM_HEAVY_TEX : 0) |
               ((s->feature_mask & G::F_MEDIUM) == 0 ? TRIM_MEDIA : 0);
+    const char* tp = getenv("HRT_GWALK_TRIMP"); /* A/B knob: "0" keeps trace_ray's generic program compiled in */
+    if (!s->w_generic && !(tp && strcmp(tp, "0") == 0)) pl.trim |= TRIM_PROGRAMS;
     if (lt && strcmp(lt, "0") == 0) pl.trim = 0;
   }
   return pl;

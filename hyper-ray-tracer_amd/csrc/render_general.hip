@@ -39,6 +39,7 @@ __global__ __launch_bounds__((BIG ? 256 : 128) * GWALK_WAVES, GWALK_WAVES)
 void render_gwalk_kernel(KParams P) {
   extern __shared__ float4 lds_scene[];
   constexpr bool MEDIA = !(TRIM & TRIM_MEDIA);
+  constexpr bool PROG = !(TRIM & TRIM_PROGRAMS);
   const G::Node* nodes = P.nodes;
   const G::Prim* prims = P.prims;
   const uint32_t lds_base = (uint32_t)(size_t)(__attribute__((address_space(3))) float4*)lds_scene;
@@ -131,13 +132,22 @@ void render_gwalk_kernel(KParams P) {
       setup = true;
     }
     if (setup) {
+#if HRT_RAY_REDERIVE
+      r.o = ps.ro;
+      r.d = ps.rd;
+      set_time(r, ps.rtime, P);
+#else
       set_ray(r, ps.ro, ps.rd, ps.rtime, P);
+#endif
       closest = inf;
       winner = G::NONE;
       gstate = G::NONE & 0x7FFFFFFFu;
       node = ps.depth_left == 0 ? G::NONE : 0u; /* max_depth 0: black without a world.hit (:478-480) */
       setup = false;
     }
+#if HRT_RAY_REDERIVE
+    set_dir(r, r.o, r.d); /* every lane: dead across shading (kernel_common.h) */
+#endif
     if constexpr (COUNT) cn.shade_slots++;
     stamp(0);
     const unsigned long long walkers = __ballot(walking);
@@ -170,7 +180,7 @@ void render_gwalk_kernel(KParams P) {
           if constexpr (COUNT) cn.prim_slots++;
           if (pend != G::NONE) {
             const float before = closest;
-            gwalk_leaf_test<MEDIA, COUNT, WMEM>(Q, nodes, prims, ws, pend, r, closest, winner, gstate, ps.pk, cn);
+            gwalk_leaf_test<MEDIA, COUNT, WMEM, PROG>(Q, nodes, prims, ws, pend, r, closest, winner, gstate, ps.pk, cn);
             if (closest != closest && before == before) {
               /* the leaf accepted a NaN t (rect.rs 0 / 0, lane.h set_noinv; in an instance's frame the world
                * ray need not be in NaN mode): the reference now passes every box and accepts the next hit at
@@ -278,15 +288,24 @@ namespace hrt {
 
 void launch_gwalk(bool count, int wmem, bool lref, int trim, const KParams& kp, int device, hipStream_t stream,
                   size_t smem) {
+  /* instantiated trims: none, media, heavy textures, both; TRIM_PROGRAMS with none (Final) or both (Cornell) */
+  if (trim & TRIM_PROGRAMS) {
+    const int base = trim & ~TRIM_PROGRAMS;
+    if (base != 0 && base != (TRIM_MEDIA | TRIM_HEAVY_TEX)) trim = base;
+  }
   if (count) {
-    if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX)) launch_g_mem<true, TRIM_MEDIA | TRIM_HEAVY_TEX>(wmem, lref, kp, device, stream, smem);
+    if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX | TRIM_PROGRAMS)) launch_g_mem<true, TRIM_MEDIA | TRIM_HEAVY_TEX | TRIM_PROGRAMS>(wmem, lref, kp, device, stream, smem);
+    else if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX)) launch_g_mem<true, TRIM_MEDIA | TRIM_HEAVY_TEX>(wmem, lref, kp, device, stream, smem);
     else if (trim == TRIM_MEDIA) launch_g_mem<true, TRIM_MEDIA>(wmem, lref, kp, device, stream, smem);
     else if (trim == TRIM_HEAVY_TEX) launch_g_mem<true, TRIM_HEAVY_TEX>(wmem, lref, kp, device, stream, smem);
+    else if (trim == TRIM_PROGRAMS) launch_g_mem<true, TRIM_PROGRAMS>(wmem, lref, kp, device, stream, smem);
     else launch_g_mem<true, 0>(wmem, lref, kp, device, stream, smem);
   } else {
-    if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX)) launch_g_mem<false, TRIM_MEDIA | TRIM_HEAVY_TEX>(wmem, lref, kp, device, stream, smem);
+    if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX | TRIM_PROGRAMS)) launch_g_mem<false, TRIM_MEDIA | TRIM_HEAVY_TEX | TRIM_PROGRAMS>(wmem, lref, kp, device, stream, smem);
+    else if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX)) launch_g_mem<false, TRIM_MEDIA | TRIM_HEAVY_TEX>(wmem, lref, kp, device, stream, smem);
     else if (trim == TRIM_MEDIA) launch_g_mem<false, TRIM_MEDIA>(wmem, lref, kp, device, stream, smem);
     else if (trim == TRIM_HEAVY_TEX) launch_g_mem<false, TRIM_HEAVY_TEX>(wmem, lref, kp, device, stream, smem);
+    else if (trim == TRIM_PROGRAMS) launch_g_mem<false, TRIM_PROGRAMS>(wmem, lref, kp, device, stream, smem);
     else launch_g_mem<false, 0>(wmem, lref, kp, device, stream, smem);
   }
 }

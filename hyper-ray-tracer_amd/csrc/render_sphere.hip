@@ -127,12 +127,21 @@ void render_basic_kernel(KParams P) {
       setup = true;
     }
     if (setup) { /* new samples and scattered rays share one pass through the ray setup (1/d, d.d) */
-      set_ray(r, ps.ro, ps.rd, ps.rtime, P); /* a scattered ray keeps the sample's shutter time */
+#if HRT_RAY_REDERIVE_SPHERE
+      r.o = ps.ro;
+      r.d = ps.rd;
+      set_time(r, ps.rtime, P); /* a scattered ray keeps the sample's shutter time */
+#else
+      set_ray(r, ps.ro, ps.rd, ps.rtime, P);
+#endif
       closest = inf;
       winner = G::NONE;
       node = ps.depth_left == 0 ? G::NONE : root; /* max_depth 0: black without a world.hit (:478-480) */
       setup = false;
     }
+#if HRT_RAY_REDERIVE_SPHERE
+    set_dir(r, r.o, r.d); /* every lane: dead across shading (kernel_common.h) */
+#endif
     /* step the walks until enough lanes have finished (lanes not walking hold node >= end).  A lane
      * whose leaf box passed holds WALK_PEND in `node` and waits; the wave runs the sphere block
      * once `batch` lanes wait (or no lane can step), instead of for every lane that needs it. */

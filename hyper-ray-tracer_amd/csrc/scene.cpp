@@ -888,6 +888,7 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
   const char* sp_env = getenv("HRT_WALK_SPLIT");
   const uint32_t H2 = G::WALK_SPLIT_HALF;
   s->w_half = 16;
+  s->w_generic = false; /* set below by the first leaf that needs trace_ray */
   if (!hybrid && !s->w_general && (s->feature_mask & ~G::F_BASIC) == 0 && sp_env && strcmp(sp_env, "1") == 0 &&
       (uint64_t)N * 16u <= H2 &&
       total >= (uint64_t)H2 + 16u * N) {
@@ -970,6 +971,7 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
           fourth = s->g_media[mi].sphere;
         }
       }
+      if (!one) s->w_generic = true;
       put4(o, q, u2f(L.begin), u2f(second), u2f((L.has_rbox ? G::GL_BOX : 0u) | L.gflags | one), u2f(skip << 2));
       put4(o, q + 16, L.rbox.mn.x, L.rbox.mn.y, L.rbox.mn.z, u2f(fourth));
       put4(o, q + 32, L.rbox.mx.x, L.rbox.mx.y, L.rbox.mx.z, u2f(L.rgroup));

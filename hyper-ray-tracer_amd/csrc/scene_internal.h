@@ -124,7 +124,8 @@ struct hrt_scene {
   bool w_device_built = false; /* ... by the device-side build (build_walk.hip) */
   bool w_regroup_pending = false; /* re-grouping left to the device build at upload */
   bool w_general = false;    /* the stream is the general-scene walk stream (layout.h; build_gwalk) */
-  uint32_t w_half = 16;      /* bytes from a node part's first 16 B to its second (16, or layout.h WALK_SPLIT_HALF) */
+  uint32_t w_half = 16;
+  bool w_generic = true;     /* general stream: a leaf's program is neither GL_ONE nor GL_MED (needs trace_ray) */      /* bytes from a node part's first 16 B to its second (16, or layout.h WALK_SPLIT_HALF) */
   uint32_t w_build_us = 0;   /* time of the re-grouping (host or device) */
   size_t off_walk = 0;
   uint32_t feature_mask = 0;
