@@ -43,7 +43,7 @@ using namespace hrt::lane;
  * lane.h set_dir) for EVERY lane at the top of every pass, the same bits again for a lane in mid-walk: they
  * are then dead across the shading code, which otherwise keeps them in registers (or scratch) for the lanes
  * still walking.  The wave runs set_dir's instructions each pass for its new rays anyway.  0: only new rays
- * (A/B; profiles/r04g_rederive_ab.txt). */
+ * (A/B; profiles/r04g_ab.txt). */
 #ifndef HRT_RAY_REDERIVE
 #define HRT_RAY_REDERIVE 1 /* the general kernel (r04: Cornell-smoke +4.9%, Final neutral, bit-identical) */
 #endif

@@ -283,7 +283,7 @@ constexpr int payload_mem() { return MEM == WM_HYB ? WM_BUF : MEM; }
 
 #ifndef HRT_HYB_ANYG
 #define HRT_HYB_ANYG 2 /* 2: the buffer loads under the exec mask of the lanes that need them (r04: C4 1/8 share at
-                          * 256 spp 5330 -> 5621 Mrays/s over 1, profiles/r04e_hyb_ab.txt); 1: skipped when no
+                          * 256 spp 5330 -> 5621 Mrays/s over 1, profiles/r04g_ab.txt); 1: skipped when no
                           * lane of the wave needs them (5291 -> 5424 over 0); 0: every lane issues them */
 #endif
 /* Both 16-B halves of the node part at `off` (walk_box).  WM_HYB: every lane issues an LDS read AND a

@@ -207,7 +207,7 @@ constexpr uint32_t WALK_NODE_BYTES = 32, WALK_PAYLOAD_BYTES = 96;
  * so consecutive node parts lie 16 B apart in each half and a 16-lane group of ds_read_b128 spreads over
  * all 16 bank slots (interleaved 32-B parts use 8).  Node parts then occupy [0, 16 N) and
  * [WALK_SPLIT_HALF, WALK_SPLIT_HALF + 16 N); payloads fill the rest (N <= 1024).  Opt-in (HRT_WALK_SPLIT=1):
- * no faster on C2 (14 024 vs 14 038 Mrays/s, profiles/r04e_split_ab.txt), so the conflicts are not what
+ * no faster on C2 (14 024 vs 14 038 Mrays/s, profiles/r04g_ab.txt), so the conflicts are not what
  * bounds the step. */
 constexpr uint32_t WALK_SPLIT_HALF = 16384;
 constexpr uint32_t WL_MOVING = 1u, WL_NOBOX = 2u;
