@@ -595,8 +595,12 @@ Aabb box_union(const Aabb& a, const Aabb& b) {
  * cost(i, j) = w(i, j) + min_k cost(i, k) + cost(k, j) over the ranges of the sequence, with w = 2 x the half
  * area (mode 1: the two child tests an inner node makes whenever a ray passes it) or half area x leaves
  * (mode 2: walk_regroup's greedy objective, minimised exactly).  Splits tie to the cut nearest the middle. */
-bool walk_regroup_dp(std::vector<WNode>& T, const std::vector<WalkLeaf>& leaves, int mode) {
-  const uint32_t n = (uint32_t)leaves.size();
+bool walk_regroup_dp(std::vector<WNode>& T, const std::vector<WalkLeaf>& all, int mode, uint32_t lo0 = 0,
+                     uint32_t hi0 = 0xFFFFFFFFu, uint32_t depth0 = 0) {
+  /* over the leaves [lo0, hi0) (default: all), the subtree's nodes appended to T at depth depth0 */
+  if (hi0 > all.size()) hi0 = (uint32_t)all.size();
+  const WalkLeaf* leaves = all.data() + lo0;
+  const uint32_t n = hi0 - lo0;
   if (n < 2 || n > 2048) return false;
   std::vector<double> A((size_t)n * (n + 1), 0.0), C((size_t)n * (n + 1), 0.0);
   std::vector<uint32_t> K((size_t)n * (n + 1), 0u);
@@ -629,13 +633,13 @@ bool walk_regroup_dp(std::vector<WNode>& T, const std::vector<WalkLeaf>& leaves,
       K[at(i, j)] = bk;
     }
   struct Range { uint32_t lo, hi, depth; };
-  std::vector<Range> todo{{0u, n, 0u}};
+  std::vector<Range> todo{{0u, n, depth0}};
   while (!todo.empty()) {
     const Range r = todo.back();
     todo.pop_back();
     const uint32_t m = r.hi - r.lo, self = (uint32_t)T.size();
     if (m == 1) {
-      T.push_back(WNode{leaves[r.lo].box, (int32_t)r.lo, self + 1, r.depth});
+      T.push_back(WNode{leaves[r.lo].box, (int32_t)(lo0 + r.lo), self + 1, r.depth});
       continue;
     }
     const uint32_t k = K[at(r.lo, r.hi)];
@@ -651,8 +655,12 @@ void walk_regroup(std::vector<WNode>& T, const std::vector<WalkLeaf>& leaves) {
   /* default: the DP (mode 1) for sequences of at most 700 leaves (O(n^3 / 6) work: ~30 ms at Random's 485),
    * the greedy split above that (and on the device, build_walk.hip) */
   const char* dp = getenv("HRT_WALK_DP");
-  const int mode = dp ? dp[0] - '0' : (leaves.size() <= 700 ? 1 : 0);
+  const int mode = dp ? dp[0] - '0' : (leaves.size() <= 700 ? 1 : 3);
   if ((mode == 1 || mode == 2) && walk_regroup_dp(T, leaves, mode)) return;
+  /* mode 3 (default above 700 leaves): the greedy split below, and each range of at most DP_SUB leaves it
+   * reaches re-grouped by the DP (mode 1) */
+  const char* ds = getenv("HRT_WALK_DP_SUB");
+  const uint32_t dp_sub = mode == 3 ? (ds ? (uint32_t)atoi(ds) : 256u) : 0u;
   struct Range { uint32_t lo, hi, depth; };
   std::vector<Range> todo{{0u, (uint32_t)leaves.size(), 0u}};
   std::vector<Aabb> pre, suf;
@@ -664,6 +672,7 @@ void walk_regroup(std::vector<WNode>& T, const std::vector<WalkLeaf>& leaves) {
       T.push_back(WNode{leaves[r.lo].box, (int32_t)r.lo, self + 1, r.depth});
       continue;
     }
+    if (n <= dp_sub && walk_regroup_dp(T, leaves, 1, r.lo, r.hi, r.depth)) continue;
     pre.resize(n);
     suf.resize(n);
     pre[0] = leaves[r.lo].box;
