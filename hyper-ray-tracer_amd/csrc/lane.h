@@ -96,19 +96,20 @@ struct KParams {
  * chunk should be long enough that claiming it and writing its partial sum are cheap next to its
  * samples, and short enough that the launch's last items (run with the device mostly idle) end soon:
  * - sphere scenes (render_basic_kernel: block claims, short passes): >= 16 samples, <= 32 chunks;
- * - general scenes (segment kernels: per-lane claims): <= 8 chunks of >= 32 samples, or of >= 16 when
- *   the main node stream is deep (> 1024 nodes: expensive samples, the tail dominates).
+ * - general scenes: <= 8 chunks of >= 32 samples; when the main node stream is deep (> 1024 nodes:
+ *   expensive samples of very uneven length) <= 64 chunks of >= 1 sample.
  * Measured: Earth+Perlin 1000 spp 11447 Mrays/s with 8 chunks vs 9703 with 32;
- * at 128 spp min 64 / 32 / 16 = 8934 / 9931 / 7930; Final 800^2 x 64 spp min 64 / 32 / 16 = 548 / 735 /
- * 928; Cornell 64 spp 6900 / 6971 / 6963. */
+ * at 128 spp min 64 / 32 / 16 = 8934 / 9931 / 7930; Cornell 64 spp 6900 / 6971 / 6963; Cornell's 1/8 share
+ * at 10000 spp flat over 8 .. 512 chunks (r04); Final 800^2 x 64 spp (r04, general walk kernel) chunk 16 /
+ * 8 / 4 / 2 / 1 = 1794 / 2300 / 2669 / 3001 / 3104 (r02, segment kernel: 64 / 32 / 16 = 548 / 735 / 928). */
 enum ChunkClass : uint32_t { CHUNK_SPHERE = 0, CHUNK_GENERAL = 1, CHUNK_GENERAL_DEEP = 2 };
 inline uint32_t chunk_class(uint32_t feature_mask, uint32_t main_nodes) {
   if ((feature_mask & ~G::F_BASIC) == 0) return CHUNK_SPHERE;
   return main_nodes > 1024u ? CHUNK_GENERAL_DEEP : CHUNK_GENERAL;
 }
 inline uint32_t sample_chunk(uint32_t spp, uint32_t cls, uint32_t cmin = 0, uint32_t cdiv = 0) {
-  if (cmin == 0) cmin = cls == CHUNK_GENERAL ? 32u : 16u;
-  if (cdiv == 0) cdiv = cls == CHUNK_SPHERE ? 32u : 8u;
+  if (cmin == 0) cmin = cls == CHUNK_GENERAL ? 32u : (cls == CHUNK_SPHERE ? 16u : 1u);
+  if (cdiv == 0) cdiv = cls == CHUNK_SPHERE ? 32u : (cls == CHUNK_GENERAL ? 8u : 64u);
   const uint32_t even = (spp + cdiv - 1) / cdiv;
   return spp <= cmin ? spp : (even > cmin ? even : cmin);
 }

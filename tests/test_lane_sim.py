@@ -93,7 +93,7 @@ CASES = [
     ("motion", 48, 27, 8, 50),           # moving spheres with their own shutter intervals (TRay.tau = time)
     ("cornell", 24, 24, 4, 2),           # depth cap
     ("cornell", 12, 12, 70, 50),         # general scene: three chunks of >= 32 samples (lane.h sample_chunk)
-    ("final", 8, 8, 40, 50),             # deep general scene (> 1024 nodes): three chunks of >= 16
+    ("final", 8, 8, 40, 50),             # deep general scene (> 1024 nodes): 40 one-sample chunks
 ]
 
 
