@@ -142,17 +142,17 @@ __device__ __forceinline__ void claim_work(const KParams& P, uint32_t lane, bool
    * stride: a division; else a binary search on pad_start) */
   uint32_t c, px;
   if (w < P.head_items) {
-    const uint32_t g = udiv_m(w, 64u * P.chunk_head, P.m_head), rem = w - g * 64u * P.chunk_head;
+    const uint32_t g = w / (64u * P.chunk_head), rem = w - g * 64u * P.chunk_head;
     c = rem >> 6;
     px = g * 64u + (rem & 63u);
   } else {
-    const uint32_t t = w - P.head_items, k = udiv_m(t, P.pad_px, P.m_pad);
+    const uint32_t t = w - P.head_items, k = t / P.pad_px;
     c = P.chunk_head + k;
     px = t - k * P.pad_px;
   }
   uint32_t lo = 0;
   if (P.tile_stride) {
-    lo = udiv_m(px, P.tile_stride, P.m_stride);
+    lo = px / P.tile_stride;
   } else {
     uint32_t hi = P.n_tiles - 1;
     while (lo < hi) {

@@ -52,10 +52,6 @@ struct KParams {
   /* render */
   uint32_t W, H, spp, max_depth, sample_offset;
   float rw1, rh1; /* RN(1 / (W - 1)), RN(1 / (H - 1)): set_pixel_rcp */
-  /* W - 1, H - 1, 1 / spp, time1 - time0 as f32 (set_pixel_rcp, the same operations as in the kernels): kernel
-   * arguments (scalar registers), not values the kernels compute once into vector registers and keep live
-   * (or spilled) across their persistent loops */
-  float w1, h1, inv_spp, time_span;
   float t_min;
   Vec3 background;
   uint64_t seed;
@@ -73,9 +69,6 @@ struct KParams {
   uint32_t chunk_head, chunk_first; /* head chunks (the first holds chunk_first samples, the rest `chunk`) */
   uint32_t pad_px;                  /* padded pixels of the call's tiles */
   uint32_t head_items;              /* pad_px x chunk_head: the head chunks' items come first (claim_work) */
-  /* claim_work's divisors 64 chunk_head, pad_px, tile_stride as reciprocals ceil(2^32 / d) (udiv_magic):
-   * scalar kernel arguments instead of reciprocals the kernel would compute into vector registers */
-  uint32_t m_head, m_pad, m_stride;
   uint32_t n_prims;
   uint32_t n_nodes;    /* node-stream entries to stage in LDS */
   uint32_t stream_len; /* FAST: length of one octant stream */
@@ -1046,20 +1039,9 @@ struct PathState {
 
 /* application.rs:444-447 + camera.rs:85-95: jitter, lens sample, shutter time */
 /* host side: the reciprocals start_sample's camera divisions use (W, H >= 2) */
-/* q = n / d for n + d < 2^32 and d >= 2 with m = udiv_magic(d): the estimate mulhi(n, m) is q or q + 1 */
-inline uint32_t udiv_magic(uint32_t d) { return d >= 2u ? (uint32_t)((0xFFFFFFFFull + d) / d) : 0u; }
-HRT_LANE_FI uint32_t udiv_m(uint32_t n, uint32_t d, uint32_t m) {
-  uint32_t q = (uint32_t)(((uint64_t)n * m) >> 32);
-  return (uint64_t)q * d > n ? q - 1u : q;
-}
-
 inline void set_pixel_rcp(KParams& P) {
   P.rw1 = 1.0f / ((float)P.W - 1.0f);
   P.rh1 = 1.0f / ((float)P.H - 1.0f);
-  P.w1 = (float)P.W - 1.0f;
-  P.h1 = (float)P.H - 1.0f;
-  P.inv_spp = 1.0f / (float)P.spp; /* application.rs:403 (after spp is set) */
-  P.time_span = P.time1 - P.time0;  /* camera.rs:93 gen_range's hi - lo */
 }
 
 HRT_LANE_FI void start_sample(const KParams& P, PathState& ps, uint32_t px, uint32_t py,
@@ -1087,13 +1069,13 @@ HRT_LANE_FI void start_sample(const KParams& P, PathState& ps, uint32_t px, uint
    *  - it is never 0: x = a m would need the >= 25 odd significant bits of m (times a) in an f32.
    * So the final RN lands on RN(x / a).  tests/native/div_rn_check.c `camera` checks every a in
    * [1, 65534] at the edge values of x (tests/test_fast_division.py). */
-  const float xu = (float)px + ps.rng.gen_f32(), aw = P.w1;
-  const float xv = (float)py + ps.rng.gen_f32(), ah = P.h1;
+  const float xu = (float)px + ps.rng.gen_f32(), aw = (float)P.W - 1.0f;
+  const float xv = (float)py + ps.rng.gen_f32(), ah = (float)P.H - 1.0f;
   const float qu = xu * P.rw1, qv = xv * P.rh1;
   float u = fmaf(fmaf(-qu, aw, xu), P.rw1, qu);
   float v = fmaf(fmaf(-qv, ah, xv), P.rh1, qv);
   Vec3 disk = random_in_unit_disk(ps.rng);
-  ps.rtime = ps.rng.gen_range_f32_span(P.time0, P.time1, P.time_span);
+  ps.rtime = ps.rng.gen_range_f32(P.time0, P.time1);
   Vec3 rdk = P.lens_radius * disk;
   Vec3 offset = P.cam_u * rdk.x + P.cam_vv * rdk.y;
   ps.ro = P.cam_origin + offset;

@@ -562,8 +562,8 @@ KParams scene_params(const hrt_scene* s, const hrt_camera* cam, const hrt_render
   kp.time1 = cam->time1;
   kp.W = p->width;
   kp.H = p->height;
-  kp.spp = p->samples;
   set_pixel_rcp(kp);
+  kp.spp = p->samples;
   kp.max_depth = p->max_depth;
   kp.sample_offset = p->sample_offset;
   kp.t_min = p->t_min;
@@ -906,9 +906,6 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     kp.chunk = chunk;
     kp.n_chunks = n_chunks;
     kp.chunk_head = n_head;
-    kp.m_head = udiv_magic(64u * n_head);
-    kp.m_pad = udiv_magic(kp.pad_px);
-    kp.m_stride = udiv_magic(kp.tile_stride);
     kp.chunk_first = first;
     kp.n_out = (uint32_t)outp;
     kp.partial = (float4*)sl.d_partial;

@@ -88,8 +88,8 @@ void render_gwalk_kernel(KParams P) {
     return;
   }
   uint32_t* const slot_lds = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(lds_scene) + P.lane_lds) + threadIdx.x;
-  const uint32_t lane = __lane_id(); /* (v_mbcnt: the value claim_work's ranks use too) */
-  const float scale = P.inv_spp; /* application.rs:403 (a kernel argument: lane.h set_pixel_rcp) */
+  const uint32_t lane = threadIdx.x & 63u;
+  const float scale = 1.0f / (float)P.spp; /* application.rs:403 */
   const float inf = __uint_as_float(0x7f800000u);
   const uint32_t end = P.walk_end;
   const float tmin_c = __builtin_canonicalizef(P.t_min);

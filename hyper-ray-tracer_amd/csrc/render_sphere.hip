@@ -74,8 +74,8 @@ void render_basic_kernel(KParams P) {
   /* the lane's Item.slot lives in LDS: a register kept across the whole item would be spilled at the
    * 80-VGPR cap (scratch written at every claim and chunk end) */
   uint32_t* const slot_lds = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(lds_scene) + P.lane_lds) + threadIdx.x;
-  const uint32_t lane = __lane_id(); /* (v_mbcnt: the value claim_work's ranks use too) */
-  const float scale = P.inv_spp; /* application.rs:403 (a kernel argument: lane.h set_pixel_rcp) */
+  const uint32_t lane = threadIdx.x & 63u;
+  const float scale = 1.0f / (float)P.spp; /* application.rs:403 */
   const float inf = __uint_as_float(0x7f800000u);
   const uint32_t end = WS ? P.walk_end : root + P.main_end * STRIDE;
   /* t_min canonicalised once: box_ce's fmaxf against it then needs no per-step quieting */

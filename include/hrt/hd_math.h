@@ -341,9 +341,8 @@ struct Rng {
   /* rand 0.8 Standard for f32: 24 random bits scaled by 2^-24 */
   HRT_HD float gen_f32() { return (float)(next_u32() >> 8) * 5.9604644775390625e-08f; }
   /* rand 0.8 UniformFloat::<f32>::sample_single(lo, hi) */
-  HRT_HD float gen_range_f32(float lo, float hi) { return gen_range_f32_span(lo, hi, hi - lo); }
-  /* with scale = hi - lo computed by the caller (the same f32 subtraction) */
-  HRT_HD float gen_range_f32_span(float lo, float hi, float scale) {
+  HRT_HD float gen_range_f32(float lo, float hi) {
+    float scale = hi - lo;
     for (;;) {
       float v12 = u2f(0x3F800000u | (next_u32() >> 9));
       float v01 = v12 - 1.0f;

@@ -186,8 +186,8 @@ int lane_sim_render(const void* blob, const hrt_blob_info* bi, const hrt_camera*
   P.time1 = cam->time1;
   P.W = p->width;
   P.H = p->height;
-  P.spp = p->samples;
   set_pixel_rcp(P);
+  P.spp = p->samples;
   P.chunk = sample_chunk(P.spp, chunk_class(bi->feature_mask, bi->main_end));
   {
     const char* ct = getenv("HRT_CHUNK_TAIL");
@@ -301,8 +301,8 @@ int lane_sim_path(const void* blob, const hrt_blob_info* bi, const hrt_camera* c
   P.time1 = cam->time1;
   P.W = p->width;
   P.H = p->height;
-  P.spp = p->samples;
   set_pixel_rcp(P);
+  P.spp = p->samples;
   P.max_depth = p->max_depth;
   P.sample_offset = p->sample_offset;
   P.t_min = p->t_min;
