@@ -419,3 +419,26 @@ def test_split_node_parts_render_the_same_frame(earth, monkeypatch):
     b, sb, s1 = _gpu_render("random", 160, 90, 16, 50, 3, earth)
     assert hrt.scene_blob(s1)[1].walk_half == 16384
     assert sa.segments == sb.segments and np.array_equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("knob", ["HRT_GWALK_MED=0", "HRT_GWALK_BIG=0", "HRT_GWALK_TRIMP=0"])
+def test_final_walk_variants_are_bit_identical(earth, monkeypatch, knob):
+    """Final through the general walk kernel's r04 variants against the default (flat one-sphere media
+    GL_MED, the 152-KB staged set of one 1024-thread workgroup, the TRIM_PROGRAMS instantiation): each knob
+    switches one back (the scene is committed under it: placement knobs act at commit), and the frame and
+    its ray count stay bit for bit the default's."""
+    w, h, spp = 96, 64, 24
+    s = hrt.preset("final", 1, earth)
+    s.commit()
+    cam = hrt.preset_camera(s.info, w, h)
+    p = hrt.params(w, h, spp, 50, 5, tuple(s.info.background))
+    a, sa = hrt.render(s, cam, p, stats=True)
+    k0 = hrt.last_launch()["kernel"]
+    assert "BIG = true" in k0 and "TRIM = 4" in k0, k0
+    k, v = knob.split("=")
+    monkeypatch.setenv(k, v)
+    s2 = hrt.preset("final", 1, earth)
+    s2.commit()
+    b, sb = hrt.render(s2, cam, p, stats=True)
+    assert sa.segments == sb.segments and np.array_equal(a, b), knob

@@ -418,3 +418,16 @@ def test_split_node_parts_equal_interleaved(sim, earth, name, monkeypatch):
     b, sb = sim_render(sim, name, 48, 27, 8, 50, 5, earth, kernel=0, cull=CULL_EXACT)
     assert sa["segments"] == sb["segments"] and sa["nodes"] == sb["nodes"]
     assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("knob", ["HRT_GWALK_MED=0", "HRT_GWALK_BIG=0"])
+def test_final_general_walk_variants(sim, earth, knob, monkeypatch):
+    """Final's general walk with a one-sphere medium as a flat program (layout.h GL_MED) and with the 152-KB
+    staged set (GWALK_LDS_BIG_BYTES), against the generic program / the 77-KB set: the same frame bit for bit
+    and the same work counters (gwalk_medium counts what trace_ray's node loop would)."""
+    a, sa = sim_render(sim, "final", 40, 40, 4, 50, 9, earth, kernel=3, cull=CULL_EXACT)
+    k, v = knob.split("=")
+    monkeypatch.setenv(k, v)
+    b, sb = sim_render(sim, "final", 40, 40, 4, 50, 9, earth, kernel=3, cull=CULL_EXACT)
+    assert sa == sb
+    assert np.array_equal(a, b)
