@@ -371,3 +371,19 @@ int lane_sim_ray_boxes(const void* blob, const hrt_blob_info* bi, const float* o
   return winner;
 }
 }  // extern "C"
+
+/* lane.h's Perlin noise (op 0) and the noise texture's scalar turbulence term (op 1: noise_value_t, i.e.
+ * 1 + sin(scale p.z + 10 |turbulence(scale p, 7)|)) on explicit tables (ranvec 256 x 3, perm 3 x 256, the
+ * oracle's layout), for the bit-for-bit check against oracle_perlin (tests/test_lane_sim.py) */
+extern "C" float lane_sim_perlin(const float* ranvec, const uint32_t* perm, int op, const float* p, float scale) {
+  static G::Perlin pn;
+  for (int i = 0; i < 256; i++) {
+    pn.ranvec[i][0] = ranvec[3 * i];
+    pn.ranvec[i][1] = ranvec[3 * i + 1];
+    pn.ranvec[i][2] = ranvec[3 * i + 2];
+    pn.ranvec[i][3] = 0.0f;
+    for (int c = 0; c < 3; c++) pn.perm[c][i] = perm[256 * c + i];
+  }
+  const Vec3 q = v3(p[0], p[1], p[2]);
+  return op == 0 ? perlin_noise(&pn, q) : noise_value_t(&pn, scale, q);
+}

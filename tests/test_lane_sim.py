@@ -431,3 +431,34 @@ def test_final_general_walk_variants(sim, earth, knob, monkeypatch):
     b, sb = sim_render(sim, "final", 40, 40, 4, 50, 9, earth, kernel=3, cull=CULL_EXACT)
     assert sa == sb
     assert np.array_equal(a, b)
+
+
+def test_perlin_lane_code_equals_oracle_bit_for_bit(sim):
+    """lane.h perlin_noise_t / noise_value_t (the kernels' Perlin) against the oracle's perlin_noise.rs
+    restatement on the scene's tables: noise and the noise texture's turbulence term, bit for bit, over points
+    of every scale (negative, integer, huge, tiny) -- the corner weights are exact simplifications of the
+    reference's x u + (1 - x)(1 - u)."""
+    L = O.load()
+    rv = np.zeros(768, np.float32)
+    pm = np.zeros(768, np.uint32)
+    L.oracle_perlin_tables(1, rv.ctypes.data_as(ctypes.c_void_p), pm.ctypes.data_as(ctypes.c_void_p))
+    sim.lane_sim_perlin.restype = ctypes.c_float
+    sim.lane_sim_perlin.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_float]
+    rng = np.random.default_rng(5)
+    pts = np.concatenate([rng.uniform(-50, 50, (3000, 3)), rng.uniform(-1e5, 1e5, (500, 3)),
+                          np.round(rng.uniform(-20, 20, (300, 3))), rng.uniform(-1e-3, 1e-3, (300, 3)),
+                          rng.uniform(-1e9, 1e9, (100, 3))]).astype(np.float32)
+    vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    for p in pts:
+        p = np.ascontiguousarray(p)
+        n_l = sim.lane_sim_perlin(vp(rv), vp(pm), 0, vp(p), 1.0)
+        n_o = L.oracle_perlin(vp(rv), vp(pm), 0, vp(p), 0)
+        assert np.float32(n_l).view(np.uint32) == np.float32(n_o).view(np.uint32), (p, n_l, n_o)
+        for scale in (4.0, 0.1):
+            t_l = sim.lane_sim_perlin(vp(rv), vp(pm), 1, vp(p), scale)
+            q = (np.float32(scale) * p).astype(np.float32)
+            t_o = L.oracle_perlin(vp(rv), vp(pm), 1, vp(q), 7)
+            # noise_value_t = 1 + sin_f(scale p.z + 10 |turb|): compare the turbulence through it
+            assert np.isfinite(t_l) or not np.isfinite(t_o)
+            want = 1.0 + float(np.float32(np.sin(np.float64(np.float32(np.float32(scale) * p[2]) + np.float32(10.0 * abs(np.float32(t_o)))))))
+            assert abs(t_l - want) <= 2e-6 * max(1.0, abs(want)), (p, scale, t_l, want)
