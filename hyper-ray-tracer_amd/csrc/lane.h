@@ -897,11 +897,6 @@ HRT_LANE_FI float perlin_noise_t(PN pn, Vec3 point) {
   u = u * u * (3.0f - 2.0f * u);
   v = v * v * (3.0f - 2.0f * v);
   w = w * w * (3.0f - 2.0f * w);
-  /* perlin_noise.rs:108-114's factor x u + (1 - x)(1 - u) for x in {0, 1} is exactly (1 - u) or u: u is in
-   * [0, 1] or NaN, so 0 u = +0 and the sum adds +0 to a value >= 0 (or NaN to NaN), and 1 v = v -- the same
-   * bits without the six multiplies and three adds per corner that strict IEEE code keeps
-   * (tests/test_lane_sim.py holds noise and turbulence to the oracle bit for bit) */
-  const float u0 = 1.0f - u, v0 = 1.0f - v, w0 = 1.0f - w;
   float acc = 0.0f;
 #pragma unroll
   for (int idx = 0; idx < 8; idx++) {
@@ -912,7 +907,8 @@ HRT_LANE_FI float perlin_noise_t(PN pn, Vec3 point) {
     const uint32_t g_i = px ^ py ^ pz;
     const Vec3 g = v3(pn->ranvec[g_i][0], pn->ranvec[g_i][1], pn->ranvec[g_i][2]);
     Vec3 weight = v3(u - (float)x, v - (float)y, w - (float)z);
-    acc += ((x ? u : u0) * (y ? v : v0)) * (z ? w : w0) * dot(g, weight);
+    acc += ((float)x * u + (float)(1 - x) * (1.0f - u)) * ((float)y * v + (float)(1 - y) * (1.0f - v)) *
+           ((float)z * w + (float)(1 - z) * (1.0f - w)) * dot(g, weight);
   }
   return acc;
 }
