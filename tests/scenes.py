@@ -92,6 +92,30 @@ def big_textured(seed=7, grid=26):
     return s
 
 
+def foggy(seed=3):
+    """Constant media of every shape the general walk stream distinguishes (constant_medium.rs:34-76), among
+    spheres, rects and a light: a world-level medium over one sphere and one over a MOVING sphere (flat GL_MED
+    programs), a medium that is a box-less List member (its program is the medium node alone), a medium over a
+    Cuboid (two boundary walks) and a fog sphere around the whole scene, as in application.rs:884-895."""
+    rng = np.random.default_rng(seed)
+    s = hrt.Scene()
+    white = s.solid(0.73, 0.73, 0.73)
+    objs = [s.sphere((0, -1000, 0), 1000, s.lambertian(s.checker(s.solid(0.2, 0.3, 0.1), white)))]
+    objs.append(s.rect(hrt.PLANE_ZX, -2, 2, -2, 2, 6.0, s.diffuse_light(s.solid(7, 7, 7))))
+    objs.append(s.constant_medium(s.sphere((0, 1, 0), 1.0, s.dielectric(1.5)), 0.8, s.solid(0.2, 0.4, 0.9)))
+    objs.append(s.constant_medium(s.moving_sphere((3, 0.8, -1), (3, 1.1, -1), 0.0, 1.0, 0.8, s.dielectric(1.5)),
+                                  1.2, s.solid(0.9, 0.3, 0.2)))
+    objs.append(s.constant_medium(s.cuboid((-4, 0, -1), (-2.5, 1.5, 0.5), white), 0.5, s.solid(0.1, 0.1, 0.1)))
+    member = s.constant_medium(s.sphere((-1.5, 0.5, 2.5), 0.5, s.dielectric(1.5)), 2.0, s.solid(0.8, 0.8, 0.2))
+    objs.append(s.list([member, s.sphere((1.5, 0.4, 2.5), 0.4, s.metal((0.7, 0.6, 0.5), 0.1))]))
+    for _ in range(12):
+        c = (float(rng.uniform(-5, 5)), 0.25, float(rng.uniform(-5, 5)))
+        objs.append(s.sphere(c, 0.25, _mat(s, rng, int(rng.integers(0, 3)))))
+    objs.append(s.constant_medium(s.sphere((0, 0, 0), 50.0, s.dielectric(1.5)), 0.002, s.solid(1, 1, 1)))
+    s.set_root(s.bvh(objs, 0.0, 1.0))
+    return s
+
+
 def camera(w, h):
     return hrt.camera((13, 2, 3), (0, 0, 0), 20.0, 0.1, 10.0, 0.0, 1.0, w, h)
 

@@ -95,3 +95,12 @@ def test_big_textured_hybrid_heavy_equals_reference_traversal(monkeypatch):
     s = scenes.big_textured()
     _reference_equal(s, 160, 90, 16, monkeypatch)
     assert s.scene_info().in_lds == 2  # the stream's staged part in LDS, the rest in global memory
+
+
+@pytest.mark.gpu
+def test_foggy_media_shapes_equal_reference_traversal(monkeypatch):
+    """Every medium shape of the general walk stream (flat one-sphere and moving-sphere media, a box-less List
+    member, a Cuboid boundary, a fog around the scene) on the GPU: the general walk kernel bit for bit equal to
+    the verbatim reference traversal and to the segment kernel (tests/test_lane_sim.py runs the same on the
+    host lanes)."""
+    _reference_equal(scenes.foggy(), 120, 72, 16, monkeypatch, ("segment",))

@@ -462,3 +462,26 @@ def test_perlin_lane_code_equals_oracle_bit_for_bit(sim):
             assert np.isfinite(t_l) or not np.isfinite(t_o)
             want = 1.0 + float(np.float32(np.sin(np.float64(np.float32(np.float32(scale) * p[2]) + np.float32(10.0 * abs(np.float32(t_o)))))))
             assert abs(t_l - want) <= 2e-6 * max(1.0, abs(want)), (p, scale, t_l, want)
+
+
+def test_foggy_scene_media_shapes(sim, monkeypatch):
+    """tests/scenes.py foggy: every medium shape the general walk stream distinguishes (flat GL_MED programs over
+    a sphere and a moving sphere, a box-less List member, a Cuboid boundary, a fog around everything).  The
+    general walk lane under EXACT equals the verbatim reference traversal of the segment lane bit for bit, and
+    equals itself with the media as generic programs (HRT_GWALK_MED=0)."""
+    import scenes
+
+    s = scenes.foggy()
+    blob, info = hrt.scene_blob(s)
+    flags = [f for _, _, f, _ in scenes.general_stream_leaves(blob, info)]
+    assert sum(1 for f in flags if f & scenes.GL_MED) == 3  # the sphere, the moving sphere, the fog
+    rc, a, sa = sim_render_scene(sim, s, 40, 24, 6, 3, CULL_EXACT)
+    assert rc == 0
+    rc, b, sb = sim_render_scene(sim, s, 40, 24, 6, 2, CULL_REFERENCE)
+    assert rc == 0
+    assert sa["segments"] == sb["segments"] and np.array_equal(a, b)
+    monkeypatch.setenv("HRT_GWALK_MED", "0")
+    s2 = scenes.foggy()
+    rc, c, sc = sim_render_scene(sim, s2, 40, 24, 6, 3, CULL_EXACT)
+    assert rc == 0
+    assert sa == sc and np.array_equal(a, c)
