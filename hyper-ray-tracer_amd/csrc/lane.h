@@ -1600,7 +1600,8 @@ HRT_LANE_FI void gwalk_leaf_test(const KParams& P, const G::Node* __restrict__ n
       return;
     }
   }
-  if constexpr (!PROG) return; /* (no such leaf: TRIM_PROGRAMS) */
+  if constexpr (!PROG && HRT_GWALK_ONE) return; /* (no such leaf: TRIM_PROGRAMS; GL_ONE leaves need the
+                                                  * generic program when built without gwalk_one) */
   /* one call site for the program (the ray: the world ray, or the innermost instance frame's) */
   TRay lr = r;
   if (flags & G::GL_BOX) { /* as gwalk_one */
