@@ -886,6 +886,9 @@ HRT_LANE Rec make_record(const KParams& P, uint32_t winner, float t, Vec3 wo, Ve
 
 /* perlin_noise.rs:80-123 over tables read through `pn`: a generic pointer, or (device, tables staged in LDS by
  * the kernel) an LDS address-space pointer, so the 8 x 4 gathers per call are ds_read, not flat loads */
+#ifndef HRT_PERLIN_SELECT
+#define HRT_PERLIN_SELECT 0
+#endif
 template <class PN>
 HRT_LANE_FI float perlin_noise_t(PN pn, Vec3 point) {
   int32_t i = sat_f2i32(floorf(point.x));
@@ -897,6 +900,13 @@ HRT_LANE_FI float perlin_noise_t(PN pn, Vec3 point) {
   u = u * u * (3.0f - 2.0f * u);
   v = v * v * (3.0f - 2.0f * v);
   w = w * w * (3.0f - 2.0f * w);
+#if HRT_PERLIN_SELECT
+  /* opt-in (unmeasured on the GPU): perlin_noise.rs:108-114's factor x u + (1 - x)(1 - u) for x in {0, 1} is
+   * exactly (1 - u) or u -- u is in [0, 1] or NaN, so 0 u = +0, the sum adds +0 to a value >= 0 (or NaN to
+   * NaN) and 1 v = v -- without the multiplies and adds strict IEEE code keeps (12 VALU per octave;
+   * tests/test_lane_sim.py checks both forms against the oracle bit for bit) */
+  const float u0 = 1.0f - u, v0 = 1.0f - v, w0 = 1.0f - w;
+#endif
   float acc = 0.0f;
 #pragma unroll
   for (int idx = 0; idx < 8; idx++) {
@@ -907,8 +917,12 @@ HRT_LANE_FI float perlin_noise_t(PN pn, Vec3 point) {
     const uint32_t g_i = px ^ py ^ pz;
     const Vec3 g = v3(pn->ranvec[g_i][0], pn->ranvec[g_i][1], pn->ranvec[g_i][2]);
     Vec3 weight = v3(u - (float)x, v - (float)y, w - (float)z);
+#if HRT_PERLIN_SELECT
+    acc += ((x ? u : u0) * (y ? v : v0)) * (z ? w : w0) * dot(g, weight);
+#else
     acc += ((float)x * u + (float)(1 - x) * (1.0f - u)) * ((float)y * v + (float)(1 - y) * (1.0f - v)) *
            ((float)z * w + (float)(1 - z) * (1.0f - w)) * dot(g, weight);
+#endif
   }
   return acc;
 }

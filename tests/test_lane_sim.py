@@ -433,11 +433,19 @@ def test_final_general_walk_variants(sim, earth, knob, monkeypatch):
     assert np.array_equal(a, b)
 
 
-def test_perlin_lane_code_equals_oracle_bit_for_bit(sim):
+@pytest.fixture(scope="module")
+def sim_perlin_select(tmp_path_factory):
+    """The lanes with the opt-in Perlin corner-weight selects (lane.h HRT_PERLIN_SELECT)."""
+    return _build_sim(tmp_path_factory, ("-DHRT_PERLIN_SELECT=1",))
+
+
+@pytest.mark.parametrize("variant", ["default", "select"])
+def test_perlin_lane_code_equals_oracle_bit_for_bit(sim, sim_perlin_select, variant):
     """lane.h perlin_noise_t / noise_value_t (the kernels' Perlin) against the oracle's perlin_noise.rs
     restatement on the scene's tables: noise and the noise texture's turbulence term, bit for bit, over points
     of every scale (negative, integer, huge, tiny) -- the corner weights are exact simplifications of the
     reference's x u + (1 - x)(1 - u)."""
+    sim = sim if variant == "default" else sim_perlin_select
     L = O.load()
     rv = np.zeros(768, np.float32)
     pm = np.zeros(768, np.uint32)
