@@ -6,10 +6,13 @@ Workload (BASELINE.json configs[1]): Scene::Random (src/application.rs:497-565, 
 (application.rs:482), counted exactly on the device.
 
   python bench.py                      # N=1, 3 timed frames after 1 warm-up
+  python bench.py --gpus N             # N ranks, started by bench.py itself (hrt/launcher.py)
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 
 Multi-GPU (north star: the image tiled across the GPUs of one node, host gather, no RCCL): one process
-per GPU; gloo carries only the control plane (barrier, max of the timings) and the host gather.
+per GPU; gloo carries only the control plane (barrier, max of the timings) and the host gather.  Without
+torchrun, `--gpus N` (N > 1, no WORLD_SIZE in the environment) makes this process a supervisor that starts
+N fresh ranks before anything touches the GPU, forwards rank 0's line and exits non-zero if any rank fails.
   --scaling tiles  (default) the frame's tile grid dealt to the ranks (hrt/tiling.py: 16-px tiles,
                    diagonal interleave); each rank renders its share in one launch per step; after the
                    timed steps the shares are gathered to rank 0 and the frame is checked bit for bit
@@ -34,6 +37,16 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "hyper-ray-tracer_amd"))
+
+if __name__ == "__main__":
+    # `--gpus N` without a launcher: start the N ranks here, before torch or the HIP library is loaded
+    from hrt import launcher
+
+    _pre = argparse.ArgumentParser(add_help=False)
+    _pre.add_argument("--gpus", type=int, default=1)
+    _gpus = _pre.parse_known_args()[0].gpus
+    if launcher.needs_spawn(_gpus):
+        sys.exit(launcher.run_ranks([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], _gpus))
 
 import torch  # noqa: E402  (first: libhrt binds to torch's HIP runtime)
 
@@ -77,6 +90,12 @@ def parse():
     ap.add_argument("--save", default="", help="write rank 0's last timed frame here (.pfm exact / .ppm 8-bit)")
     ap.add_argument("--one-device", action="store_true",
                     help="every rank on GPU 0 (rehearsal of the N > 1 path on a one-GPU box; not a scaling figure)")
+    ap.add_argument("--rehearsal", choices=["turns", "concurrent"], default="turns",
+                    help="--one-device timing: ranks launch their shares in turns (each launch alone on the GPU, "
+                         "as on separate GPUs), or all at once (the ranks' persistent grids then contend for the "
+                         "one GPU, DESIGN.md section 9)")
+    ap.add_argument("--allow-knobs", action="store_true",
+                    help="print the line even when A/B environment knobs of the library are set (never for a headline)")
     ap.add_argument("--share", type=int, default=1,
                     help="one process: render rank 0's share of an N-way tile split (one GPU's part of an N-GPU frame)")
     ap.add_argument("--launch-record", default="",
@@ -109,6 +128,32 @@ def usable_cpus():
     except (OSError, ValueError):
         pass
     return max(1, min(n, int(math.floor(quota)) if quota else n)), quota
+
+
+def rank_devices(dev, rank, local, world):
+    """Every rank's GPU: its PCI address (domain:bus:device) and UUID, gathered to all ranks over gloo, so the
+    line shows how many distinct devices the N ranks really ran on."""
+    pr = torch.cuda.get_device_properties(dev)
+    me = {"rank": rank, "local_rank": local, "device": dev.index, "name": pr.name,
+          "pci": f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}", "uuid": str(pr.uuid)}
+    if world == 1:
+        return [me]
+    import torch.distributed as dist
+
+    allv = [None] * world
+    dist.all_gather_object(allv, me)
+    return allv
+
+
+def distinct_devices(devices):
+    return len({(d["pci"], d["uuid"]) for d in devices})
+
+
+def knob_report(launch):
+    """The library's A/B environment knobs in effect (hrt_last_launch.knobs: every HRT_* variable the library
+    read that is set), as a list of NAME=value."""
+    k = (launch or {}).get("knobs") or ""
+    return [x for x in k.split(";") if x]
 
 
 SCENE_LABEL = {  # BASELINE.json configs
@@ -328,10 +373,21 @@ def main():
             sys.stdout.flush()
             os.dup2(saved, 1)
             os.close(saved)
+    if args.gpus > 1 and world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE is {world}")
     if args.one_device:
         local = 0
+    n_dev = torch.cuda.device_count()
+    if local >= n_dev:
+        raise SystemExit(f"bench.py rank {rank}: LOCAL_RANK {local} but {n_dev} GPU(s) visible "
+                         "(--one-device rehearses N ranks on one GPU)")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    devices = rank_devices(dev, rank, local, world)
+    if world > 1 and not args.one_device and distinct_devices(devices) != world:
+        raise SystemExit(f"bench.py: {world} ranks run on {distinct_devices(devices)} distinct devices "
+                         "(--one-device rehearses N ranks on one GPU)")
+    turns = args.one_device and world > 1 and args.rehearsal == "turns"
 
     scene = hrt.preset(args.preset, 1, earth_image())
     scene.commit(local)
@@ -378,6 +434,15 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(args.steps):
+        if turns:  # --one-device rehearsal: rank r launches its share while the others wait at the barrier
+            for r in range(world):
+                if r == rank:
+                    ev[k][0].record(stream)
+                    hrt.render_tiles_device(scene, cam, p, tiles, out.data_ptr(), stream.cuda_stream)
+                    ev[k][1].record(stream)
+                    torch.cuda.synchronize(dev)
+                barrier()
+            continue
         ev[k][0].record(stream)
         hrt.render_tiles_device(scene, cam, p, tiles, out.data_ptr(), stream.cuda_stream)
         ev[k][1].record(stream)
@@ -389,6 +454,10 @@ def main():
     dt = time.perf_counter() - t0
     scene.synchronize()  # raises if the walk watchdog stopped any timed launch (incomplete frame)
     launch = hrt.last_launch()  # what the timed steps ran: kernel, persistent grid, occupancy, VGPRs, scratch
+    knobs = knob_report(launch)
+    if knobs and not args.allow_knobs:
+        raise SystemExit(f"bench.py: library A/B knobs set in the environment ({', '.join(knobs)}): a headline line "
+                         "runs the default library; pass --allow-knobs for an A/B line")
     if args.launch_record:
         os.makedirs(os.path.dirname(os.path.abspath(args.launch_record)), exist_ok=True)
         with open(args.launch_record, "w") as fh:
@@ -473,7 +542,7 @@ def main():
             "metric": "Mrays/sec at 1920x1080, 500 spp, RTIOW final scene; per-pixel Linf vs CPU ref",
             "value": round(value, 2),
             "unit": "Mrays/s",
-            "n_gpus": 1 if args.one_device else world,
+            "n_gpus": distinct_devices(devices),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 2),
@@ -495,6 +564,10 @@ def main():
                 "cull_mode": {0: "reference", 1: "slab (approximate)", 2: "exact (reference test + provably safe culling)"}[si.cull_mode],
             },
             "launch": launch,
+            "ranks": world,
+            "devices": devices,
+            "launcher": ("bench.py --gpus (hrt/launcher.py)" if os.environ.get("HRT_BENCH_SPAWNED")
+                         else ("torch.distributed.run" if world > 1 else "single process")),
             "parity": parity,
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -503,11 +576,14 @@ def main():
             line["delivery"] = deliv
         if frame_check is not None:
             line["frame_check"] = frame_check
+        if knobs:
+            line["knobs"] = knobs
         if args.one_device and world > 1:
-            line["ranks"] = world
-            line["rehearsal"] = True
+            line["rehearsal"] = args.rehearsal
             line["note"] = (f"--one-device: all {world} ranks shared GPU 0 (a rehearsal of the multi-GPU path, not a "
-                            "scaling figure): n_gpus counts distinct devices")
+                            "scaling figure): n_gpus counts distinct devices; "
+                            + ("the ranks launched their shares in turns, each alone on the GPU" if turns else
+                               "the ranks launched at once and their persistent grids contended for the GPU"))
         print(json.dumps(line), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

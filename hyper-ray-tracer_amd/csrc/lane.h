@@ -135,6 +135,23 @@ inline void chunk_plan(uint32_t spp, uint32_t c, uint32_t levels, uint32_t& n_he
   n_tail = 2u * L;
 }
 
+/* The chunk schedule of a render: sample_chunk + chunk_plan, with the chunk doubled while the partial sums
+ * of a whole frame (n_chunks x W x H x 16 B) would exceed CHUNK_PARTIAL_BUDGET (one-sample chunks
+ * of a deep general scene at 3840x2160 would need 8.5 GB per in-flight launch).  The cap depends on the FULL
+ * image size, never on the tile split, so every split still sums a pixel's samples in the same chunks.  No
+ * BASELINE configuration reaches it (C4, the largest: 40 chunks x 133 MB = 5.3 GB). */
+constexpr unsigned long long CHUNK_PARTIAL_BUDGET = 6ull << 30;
+inline void frame_chunks(uint32_t spp, uint32_t cls, uint32_t W, uint32_t H, uint32_t cmin, uint32_t cmax, uint32_t levels,
+                         uint32_t& c, uint32_t& n_head, uint32_t& first, uint32_t& n_tail) {
+  c = sample_chunk(spp, cls, cmin, cmax);
+  const unsigned long long frame = (unsigned long long)W * H * 16u;
+  for (;;) {
+    chunk_plan(spp, c, levels, n_head, first, n_tail);
+    if (n_head + n_tail <= 1 || (unsigned long long)(n_head + n_tail) * frame <= CHUNK_PARTIAL_BUDGET || c >= spp) return;
+    c = c > spp / 2 ? spp : 2 * c;
+  }
+}
+
 /* samples [s0, s1) of chunk k */
 HRT_LANE_FI void chunk_range(const KParams& P, uint32_t k, uint32_t& s0, uint32_t& s1) {
   if (k < P.chunk_head) {
@@ -607,9 +624,7 @@ struct PathKey {
   uint32_t segment;
 };
 
-#ifndef HRT_MEDIUM_PAIR
-#define HRT_MEDIUM_PAIR 1 /* 0: a one-sphere medium boundary takes the two boundary walks (A/B) */
-#endif
+/* HRT_MEDIUM_PAIR: layout.h */
 
 /* A medium's boundary that is ONE sphere / moving sphere (Medium.sphere; its record p0, p1, p2 in registers):
  * both boundary queries of constant_medium.rs:37-48 from one evaluation of the quadratic (sphere_pair_at),

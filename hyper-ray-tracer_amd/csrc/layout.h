@@ -17,6 +17,13 @@
 #include <stdint.h>
 
 namespace hrt {
+/* 0 (A/B build): a one-sphere medium boundary takes the two boundary walks of constant_medium.rs:37-48 in
+ * every kernel; the general stream then emits no GL_MED leaves either (scene.cpp), so the build is a clean
+ * comparison.  1: both queries from one evaluation of the quadratic (lane.h sphere_pair_at). */
+#ifndef HRT_MEDIUM_PAIR
+#define HRT_MEDIUM_PAIR 1
+#endif
+
 namespace gpu {
 
 constexpr uint32_t NONE = 0xFFFFFFFFu;

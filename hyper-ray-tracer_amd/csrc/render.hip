@@ -404,7 +404,7 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
    * levels (w_hot) when it exceeds the LDS budget */
   if (!pl.full && !pl.fast && pl.cull == G::CULL_EXACT) pl.smem = s->w_hot ? s->w_hot : s->w_end;
   pl.lds = (flags & HRT_RENDER_NO_LDS) == 0 && pl.smem <= (pl.fast ? LDS_FAST_MAX : LDS_SCENE_MAX);
-  const char* k = getenv("HRT_KERNEL");
+  const char* k = knob_env("HRT_KERNEL");
   /* General scenes run the segment-at-a-time kernel by default; render_full_kernel (persistent walks)
    * is opt-in (HRT_KERNEL=persistent) until it has been measured and validated on the GPU.  Sphere
    * scenes can be sent to the segment kernel for diagnostics (HRT_KERNEL=general). */
@@ -412,11 +412,11 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
   pl.general = (k && strcmp(k, "general") == 0) || s->media_nested || (pl.full && !persistent);
   /* render_kernel<FULL>: node stream + primitives in LDS when they fit three 256-thread workgroups per
    * CU (HRT_GEN_LDS=0: global memory, for A/B) */
-  const char* gl = getenv("HRT_GEN_LDS");
+  const char* gl = knob_env("HRT_GEN_LDS");
   if (pl.general && pl.full && (pl.smem > LDS_GEN_MAX || (gl && strcmp(gl, "0") == 0))) pl.lds = false;
-  const char* gw = getenv("HRT_GEN_WAVES_RT"); /* A/B override: 3 or 4 */
+  const char* gw = knob_env("HRT_GEN_WAVES_RT"); /* A/B override: 3 or 4 */
   pl.gen_waves = gw ? (strcmp(gw, "3") == 0 ? 3 : 4) : ((s->feature_mask & G::F_NOISE) && pl.lds ? 3 : 4);
-  const char* lt = getenv("HRT_GEN_TRIM"); /* A/B knob: "0" keeps the all-feature instantiation */
+  const char* lt = knob_env("HRT_GEN_TRIM"); /* A/B knob: "0" keeps the all-feature instantiation */
   /* instantiated: all features (0), no noise / image textures (HEAVY_TEX: Cornell-smoke 124 VGPRs, no
    * spills, +1.9%), neither those nor media (Cornell: 92 VGPRs, 5 waves/SIMD, +19%).  Trimming the
    * medium branch alone measured -0.6 / -1% (Earth+Perlin, simple-light), so it is not built. */
@@ -431,7 +431,7 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
     pl.smem = s->w_hot ? s->w_hot : s->w_end;
     pl.lds = (flags & HRT_RENDER_NO_LDS) == 0 && pl.smem <= LDS_SCENE_MAX;
     const size_t perlin = s->perlin.size() * sizeof(G::Perlin);
-    const char* pe = getenv("HRT_PERLIN_LDS"); /* A/B knob: "0" keeps the Perlin tables in global memory */
+    const char* pe = knob_env("HRT_PERLIN_LDS"); /* A/B knob: "0" keeps the Perlin tables in global memory */
     pl.perlin_lds = pl.lds && perlin > 0 && pl.smem + perlin <= LDS_SCENE_MAX && !(pe && strcmp(pe, "0") == 0);
     if (pl.perlin_lds) pl.smem += perlin;
   }
@@ -457,17 +457,17 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
     /* a hybrid general stream's staged part may take one 1024-thread workgroup's LDS (GWALK_LDS_BIG_BYTES) */
     pl.gwalk_mem = no_lds || walk > (s->w_hot ? (size_t)G::GWALK_LDS_BIG_BYTES : LDS_SCENE_MAX) ? WM_BUF
                                                                                              : (s->w_hot ? WM_HYB : WM_LDS);
-    const char* lr = getenv("HRT_GWALK_LREF"); /* A/B knob: "0" keeps the reference stream in global memory */
+    const char* lr = knob_env("HRT_GWALK_LREF"); /* A/B knob: "0" keeps the reference stream in global memory */
     pl.gwalk_lref = pl.gwalk_mem == WM_LDS && walk + ref <= LDS_SCENE_MAX && !(lr && strcmp(lr, "0") == 0);
     pl.smem = pl.gwalk_mem == WM_BUF ? 0 : walk + (pl.gwalk_lref ? ref : 0);
     const size_t perlin = s->perlin.size() * sizeof(G::Perlin);
-    const char* pe = getenv("HRT_PERLIN_LDS");
+    const char* pe = knob_env("HRT_PERLIN_LDS");
     pl.perlin_lds = pl.gwalk_lref && perlin > 0 && pl.smem + perlin <= LDS_SCENE_MAX && !(pe && strcmp(pe, "0") == 0);
     if (pl.perlin_lds) pl.smem += perlin;
     pl.lds = pl.gwalk_mem != WM_BUF;
     pl.trim = ((s->feature_mask & (G::F_NOISE | G::F_IMAGE)) == 0 ? TRIM_HEAVY_TEX : 0) |
               ((s->feature_mask & G::F_MEDIUM) == 0 ? TRIM_MEDIA : 0);
-    const char* tp = getenv("HRT_GWALK_TRIMP"); /* A/B knob: "0" keeps trace_ray's generic program compiled in */
+    const char* tp = knob_env("HRT_GWALK_TRIMP"); /* A/B knob: "0" keeps trace_ray's generic program compiled in */
     if (!s->w_generic && !(tp && strcmp(tp, "0") == 0)) pl.trim |= TRIM_PROGRAMS;
     if (lt && strcmp(lt, "0") == 0) pl.trim = 0;
   }
@@ -530,9 +530,17 @@ void launch_any(const hrt_scene* s, const Plan& pl, const KParams& kp, hipStream
  *   HRT_POSTPONE   a wave leaves the walk to shade once this many lanes have finished theirs;
  *   HRT_PRIM_BATCH the wave runs its primitive tests once this many lanes wait for one. */
 uint32_t env_knob(const char* name, uint32_t dflt) {
-  const char* e = getenv(name);
+  const char* e = knob_env(name);
   const long x = e ? strtol(e, nullptr, 10) : 0;
   return (uint32_t)(x >= 1 && x <= 64 ? x : dflt);
+}
+
+/* A render's sample chunks (lane.h frame_chunks): its inputs are the spp, the scene's class, the full image
+ * size and the scene's options (hrt_scene_options), never the environment. */
+void chunk_schedule(const hrt_scene* s, const hrt_render_params* p, uint32_t& chunk, uint32_t& n_head, uint32_t& first,
+                    uint32_t& n_tail) {
+  frame_chunks(p->samples, chunk_class(s->feature_mask, s->main_end), p->width, p->height, s->opts.chunk_min,
+               s->opts.chunk_max, s->opts.chunk_uniform ? 0u : 32u, chunk, n_head, first, n_tail);
 }
 
 /* scene + camera + render knobs of a launch (work-distribution fields are set by the caller) */
@@ -778,6 +786,21 @@ void device_release(hrt_scene* s) {
 
 }  // namespace hrt
 
+namespace hrt {
+/* a device buffer freed on every exit path (the debug entry points throw through hip_check) */
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  explicit DevBuf(size_t bytes) { hip_check(hipMalloc((void**)&p, bytes), "hipMalloc(debug)"); }
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+};
+
+}  // namespace hrt
+
 extern "C" {
 
 hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hrt_render_params* p,
@@ -794,14 +817,8 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
      * frame 14243 / 14489 / 14489 / 14338 / 13930).  The rule depends on spp and
      * the scene's feature class only, so every tile split sums a pixel's samples in the same chunks. */
     const uint32_t spp = p->samples;
-    const char* cm = getenv("HRT_CHUNK_MIN"); /* A/B knob: the smallest chunk (default 16 / 32) */
-    const uint32_t cmin = cm && atoi(cm) > 0 ? (uint32_t)atoi(cm) : 0u;
-    const char* cd = getenv("HRT_CHUNK_DIV"); /* A/B knob: at most this many chunks (default 32 / 8) */
-    const uint32_t cdiv = cd && atoi(cd) > 0 ? (uint32_t)atoi(cd) : 0u;
-    const uint32_t chunk = sample_chunk(spp, chunk_class(s->feature_mask, s->main_end), cmin, cdiv);
-    const char* ct = getenv("HRT_CHUNK_TAIL"); /* A/B knob: halving levels of the tail ("0" = uniform chunks) */
-    uint32_t n_head = 0, first = 0, n_tail = 0;
-    chunk_plan(spp, chunk, ct ? (uint32_t)atoi(ct) : 32u, n_head, first, n_tail);
+    uint32_t chunk = 0, n_head = 0, first = 0, n_tail = 0;
+    chunk_schedule(s, p, chunk, n_head, first, n_tail);
     const uint32_t n_chunks = n_head + n_tail;
     std::vector<G::TileDev> td(n_tiles);
     uint64_t pad = 0, outp = 0;
@@ -822,7 +839,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     if (n_tiles > 1) {
       uint64_t mx = 0;
       for (uint32_t i = 0; i < n_tiles; i++) mx = std::max<uint64_t>(mx, (uint64_t)((td[i].w + 7) / 8) * ((td[i].h + 7) / 8) * 64);
-      const char* ts = getenv("HRT_TILE_STRIDE"); /* A/B knob: "0" keeps the binary search */
+      const char* ts = knob_env("HRT_TILE_STRIDE"); /* A/B knob: "0" keeps the binary search */
       if (mx * n_tiles <= pad + pad / 8 && mx * n_tiles * n_chunks < 0xF0000000ull && !(ts && strcmp(ts, "0") == 0)) {
         stride = (uint32_t)mx;
         for (uint32_t i = 0; i < n_tiles; i++) td[i].pad_start = i * stride;
@@ -896,7 +913,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
      * per lane (Cornell 1024^2 x 128: 2) blocks unbalance the waves (-6%).
      * HRT_CLAIM_FINE (A/B knob): claim the last that many items per lane, in every kernel */
     const bool sphere_kernel = (!pl.full && !pl.fast && !pl.general) || pl.gwalk; /* block claims */
-    const char* cf = getenv("HRT_CLAIM_FINE");
+    const char* cf = knob_env("HRT_CLAIM_FINE");
     const uint64_t work = pad * n_chunks;
     const uint64_t fine = cf ? strtoull(cf, nullptr, 10) : (sphere_kernel ? 0u : work);
     kp.claim_fine = (uint32_t)(work > fine ? work - fine : 0);
@@ -1109,10 +1126,10 @@ hrt_status hrt_debug_trace_path(hrt_scene* s, const hrt_camera* cam, const hrt_r
     const Plan pl = plan(s, cam, p->flags);
     KParams kp = scene_params(s, cam, p, pl);
     size_t bytes = (9 * (size_t)max_segments + 3) * sizeof(float);
-    float* d_out = nullptr;
-    uint32_t* d_n = nullptr;
-    hip_check(hipMalloc((void**)&d_out, bytes), "hipMalloc");
-    hip_check(hipMalloc((void**)&d_n, 4), "hipMalloc");
+    DevBuf<float> out_buf(bytes);
+    DevBuf<uint32_t> n_buf(4);
+    float* d_out = out_buf.p;
+    uint32_t* d_n = n_buf.p;
     if (pl.fast) hipLaunchKernelGGL((debug_path_kernel<G::CULL_SLAB, false, true>), dim3(1), dim3(64), 0, 0, kp, x, y, sample, d_out, max_segments, d_n);
     else if ((pl.full || pl.heavy) && pl.cull == G::CULL_EXACT) hipLaunchKernelGGL((debug_path_kernel<G::CULL_EXACT, true, false>), dim3(1), dim3(64), 0, 0, kp, x, y, sample, d_out, max_segments, d_n);
     else if (pl.cull == G::CULL_EXACT) hipLaunchKernelGGL((debug_path_kernel<G::CULL_EXACT, false, false>), dim3(1), dim3(64), 0, 0, kp, x, y, sample, d_out, max_segments, d_n);
@@ -1123,8 +1140,6 @@ hrt_status hrt_debug_trace_path(hrt_scene* s, const hrt_camera* cam, const hrt_r
     hip_check(hipGetLastError(), "debug_path_kernel launch");
     hip_check(hipMemcpy(out, d_out, bytes, hipMemcpyDeviceToHost), "hipMemcpy");
     hip_check(hipMemcpy(n_segments, d_n, 4, hipMemcpyDeviceToHost), "hipMemcpy");
-    (void)hipFree(d_out);
-    (void)hipFree(d_n);
   });
 }
 
@@ -1142,20 +1157,26 @@ hrt_status hrt_debug_box_test(int32_t form, int32_t on_device, const float* boxe
                                                : box_pair<false>(boxes, rays, b, q, tmin, tmax);
       return;
     }
-    float *db = nullptr, *dr = nullptr;
-    uint8_t* dout = nullptr;
-    hip_check(hipMalloc((void**)&db, (size_t)n_boxes * 32), "hipMalloc");
-    hip_check(hipMalloc((void**)&dr, (size_t)n_rays * 24), "hipMalloc");
-    hip_check(hipMalloc((void**)&dout, n), "hipMalloc");
+    /* on the calling thread's current device (hipSetDevice / torch.cuda.set_device), like hrt_debug_device_math */
+    DevBuf<float> b_buf((size_t)n_boxes * 32), r_buf((size_t)n_rays * 24);
+    DevBuf<uint8_t> o_buf(n);
+    float *db = b_buf.p, *dr = r_buf.p;
+    uint8_t* dout = o_buf.p;
     hip_check(hipMemcpy(db, boxes, (size_t)n_boxes * 32, hipMemcpyHostToDevice), "hipMemcpy");
     hip_check(hipMemcpy(dr, rays, (size_t)n_rays * 24, hipMemcpyHostToDevice), "hipMemcpy");
     hipLaunchKernelGGL(box_test_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, 0, form, db, n_boxes, dr, n_rays,
                        tmin, tmax, dout);
     hip_check(hipGetLastError(), "box_test_kernel launch");
     hip_check(hipMemcpy(out, dout, n, hipMemcpyDeviceToHost), "hipMemcpy");
-    (void)hipFree(db);
-    (void)hipFree(dr);
-    (void)hipFree(dout);
+  });
+}
+
+hrt_status hrt_debug_sample_chunks(hrt_scene* s, const hrt_render_params* p, uint32_t* out4) {
+  return hguard([&] {
+    if (!s || !p || !out4) throw HipError{HRT_ERR_INVALID_ARG, "hrt_debug_sample_chunks: null argument"};
+    if (p->samples == 0) throw HipError{HRT_ERR_INVALID_ARG, "hrt_debug_sample_chunks: no samples"};
+    if (!s->committed) flatten_scene(s);
+    chunk_schedule(s, p, out4[0], out4[1], out4[2], out4[3]);
   });
 }
 
@@ -1164,6 +1185,7 @@ hrt_status hrt_last_launch(hrt_launch_info* out) {
     if (!out) throw HipError{HRT_ERR_INVALID_ARG, "hrt_last_launch: null pointer"};
     if (!t_has_launch) throw HipError{HRT_ERR_STATE, "hrt_last_launch: no launch on this thread yet"};
     *out = t_last_launch;
+    snprintf(out->knobs, sizeof(out->knobs), "%s", knobs_in_effect().c_str());
   });
 }
 
@@ -1171,18 +1193,13 @@ hrt_status hrt_debug_device_math(int32_t op, const float* x, const float* y, flo
   return hguard([&] {
     if (!x || !out || op < 0 || op > 7) throw HipError{HRT_ERR_INVALID_ARG, "bad argument"};
     if (n == 0) return;
-    float *dx = nullptr, *dy = nullptr, *dout = nullptr;
-    hip_check(hipMalloc((void**)&dx, n * 4), "hipMalloc");
-    hip_check(hipMalloc((void**)&dout, n * 4), "hipMalloc");
-    if (y) hip_check(hipMalloc((void**)&dy, n * 4), "hipMalloc");
+    DevBuf<float> x_buf((size_t)n * 4), o_buf((size_t)n * 4), y_buf(y ? (size_t)n * 4 : 4);
+    float *dx = x_buf.p, *dy = y ? y_buf.p : nullptr, *dout = o_buf.p;
     hip_check(hipMemcpy(dx, x, n * 4, hipMemcpyHostToDevice), "hipMemcpy");
     if (y) hip_check(hipMemcpy(dy, y, n * 4, hipMemcpyHostToDevice), "hipMemcpy");
     hipLaunchKernelGGL(math_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, op, dx, dy, dout, n);
     hip_check(hipGetLastError(), "math_kernel launch");
     hip_check(hipMemcpy(out, dout, n * 4, hipMemcpyDeviceToHost), "hipMemcpy");
-    (void)hipFree(dx);
-    (void)hipFree(dout);
-    if (dy) (void)hipFree(dy);
   });
 }
 

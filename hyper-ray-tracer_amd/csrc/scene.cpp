@@ -200,11 +200,10 @@ uint32_t build_bvh(hrt_scene* s, std::vector<uint32_t> objects, float t0, float 
                    [](const std::pair<float, uint32_t>& a, const std::pair<float, uint32_t>& b) {
                      return a.first < b.first;
                    });
-  /* HRT_BVH_TIES=reverse (diagnostics): sorts of more than 20 objects put equal keys in the reverse
+  /* hrt_scene_options.bvh_ties = 1 (diagnostics): sorts of more than 20 objects put equal keys in the reverse
    * order, another order Rust's pdqsort could produce; tests/test_gpu_configs.py renders both trees to
    * show what the unpinned tie order changes (hrt_scene_info.bvh_tied_sorts) */
-  const char* ties = getenv("HRT_BVH_TIES");
-  if (ties && strcmp(ties, "reverse") == 0 && keys.size() > 20)
+  if (s->opts.bvh_ties == 1 && keys.size() > 20)
     for (size_t i = 0; i < keys.size();) {
       size_t j = i + 1;
       while (j < keys.size() && keys[j].first == keys[i].first) j++;
@@ -559,7 +558,7 @@ void build_fast(hrt_scene* s) {
  *
  * The leaves are the reference stream's leaves (K_BOX_PRIM: a BvhNode leaf, K_PRIM: a List member) in
  * the reference's pre-order, so the walk tests the same primitives in the same order as BvhNode::hit
- * (bvh_node.rs:104-127).  Above them, by default (HRT_WALK_TREE unset or "sah"), the inner boxes are
+ * (bvh_node.rs:104-127).  Above them, by default (hrt_scene_options.walk_tree = 0), the inner boxes are
  * RE-GROUPED: a top-down surface-area split of the fixed leaf sequence (each range cut where
  * SA(left) n_left + SA(right) n_right is least).  The reference's own hierarchy splits on the longest
  * axis of its node's box, which the r = 1000 ground sphere makes the y axis at every level that holds
@@ -567,7 +566,7 @@ void build_fast(hrt_scene* s) {
  * the re-grouped tree puts the ground sphere alone under the root (64.4 -> ~53 node visits per ray on
  * Random in a host simulation).  Any hierarchy over the same leaf sequence whose boxes hold their
  * leaves' boxes gives the reference's result.  The reference hierarchy itself is
- * kept (HRT_WALK_TREE=reference) for A/B, and whenever a leaf has no box or a box that is not a finite
+ * kept (walk_tree = 1) for A/B, and whenever a leaf has no box or a box that is not a finite
  * well-formed interval. */
 /* walk_box.h ce_floored on an Aabb */
 bool box_ce_floored(const Aabb& bx, float* C, float* E, Aabb* fb) {
@@ -654,12 +653,12 @@ bool walk_regroup_dp(std::vector<WNode>& T, const std::vector<WalkLeaf>& all, in
 void walk_regroup(std::vector<WNode>& T, const std::vector<WalkLeaf>& leaves) {
   /* default: the DP (mode 1) for sequences of at most 700 leaves (O(n^3 / 6) work: ~30 ms at Random's 485),
    * the greedy split above that (and on the device, build_walk.hip) */
-  const char* dp = getenv("HRT_WALK_DP");
+  const char* dp = knob_env("HRT_WALK_DP");
   const int mode = dp ? dp[0] - '0' : (leaves.size() <= 700 ? 1 : 3);
   if ((mode == 1 || mode == 2) && walk_regroup_dp(T, leaves, mode)) return;
   /* mode 3 (default above 700 leaves): the greedy split below, and each range of at most DP_SUB leaves it
    * reaches re-grouped by the DP (mode 1) */
-  const char* ds = getenv("HRT_WALK_DP_SUB");
+  const char* ds = knob_env("HRT_WALK_DP_SUB");
   const uint32_t dp_sub = mode == 3 ? (ds ? (uint32_t)atoi(ds) : 256u) : 0u;
   struct Range { uint32_t lo, hi, depth; };
   std::vector<Range> todo{{0u, (uint32_t)leaves.size(), 0u}};
@@ -824,10 +823,10 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
   for (const WNode& w : T) total += G::WALK_NODE_BYTES + (w.leaf >= 0 ? PB : 0);
   need(total < (1ull << 30), HRT_ERR_UNSUPPORTED, "scene too large for the walk stream");
   std::vector<uint32_t> addr(N), paddr(N, 0);
-  const char* hot_env = getenv("HRT_WALK_HOT"); /* "0": no LDS-staged top levels (A/B) */
+  const char* hot_env = knob_env("HRT_WALK_HOT"); /* "0": no LDS-staged top levels (A/B) */
   /* the staged budget: general streams twice the sphere kernel's (layout.h GWALK_LDS_BIG_BYTES; HRT_GWALK_BIG=0
    * keeps LDS_SCENE_MAX_BYTES, A/B) */
-  const char* big_env = getenv("HRT_GWALK_BIG");
+  const char* big_env = knob_env("HRT_GWALK_BIG");
   const uint32_t budget = s->w_general && !(big_env && strcmp(big_env, "0") == 0) ? G::GWALK_LDS_BIG_BYTES
                                                                                    : G::LDS_SCENE_MAX_BYTES;
   const bool hybrid = total > G::LDS_SCENE_MAX_BYTES && !(hot_env && strcmp(hot_env, "0") == 0);
@@ -837,8 +836,8 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
    * are those a ray is likeliest to reach (largest parent box surface first; HRT_WALK_HOTSEL=depth: the
    * top levels breadth first), and the global node parts stay dense in pre-order with every payload
    * after them (HRT_WALK_PAYLOADS=inline: each payload behind its leaf) */
-  const char* hotsel = getenv("HRT_WALK_HOTSEL");
-  const char* pl = getenv("HRT_WALK_PAYLOADS");
+  const char* hotsel = knob_env("HRT_WALK_HOTSEL");
+  const char* pl = knob_env("HRT_WALK_PAYLOADS");
   const bool by_area = !(hotsel && strcmp(hotsel, "depth") == 0);
   const bool apart = !(pl && strcmp(pl, "inline") == 0);
   if (hybrid) {
@@ -894,7 +893,7 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
   uint32_t END = off;
   /* split node parts (layout.h WALK_SPLIT_HALF), opt-in (HRT_WALK_SPLIT=1): sphere streams staged whole in
    * LDS that fill the space between the two halves with payloads */
-  const char* sp_env = getenv("HRT_WALK_SPLIT");
+  const char* sp_env = knob_env("HRT_WALK_SPLIT");
   const uint32_t H2 = G::WALK_SPLIT_HALF;
   s->w_half = 16;
   s->w_generic = false; /* set below by the first leaf that needs trace_ray */
@@ -973,8 +972,9 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
         const uint32_t k0 = (s->g_nodes[L.begin].kp >> 24) & G::KIND_MASK;
         const uint32_t k1 = (s->g_nodes[L.begin + 1].kp >> 24) & G::KIND_MASK;
         const uint32_t mi = s->g_nodes[L.begin + 1].kp & 0xFFFFFFu;
-        const char* me = getenv("HRT_GWALK_MED"); /* "0": media leaves run trace_ray (A/B) */
-        if (k0 == G::K_BOX && k1 == G::K_MEDIUM && s->g_media[mi].sphere != G::NONE && !(me && strcmp(me, "0") == 0)) {
+        const char* me = knob_env("HRT_GWALK_MED"); /* "0": media leaves run trace_ray (A/B) */
+        if (HRT_MEDIUM_PAIR && k0 == G::K_BOX && k1 == G::K_MEDIUM && s->g_media[mi].sphere != G::NONE &&
+            !(me && strcmp(me, "0") == 0)) {
           one = G::GL_MED;
           second = mi;
           fourth = s->g_media[mi].sphere;
@@ -1288,9 +1288,9 @@ std::vector<WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<WNode>* ref_t
     start.push_back(f.begin);
     leaves.push_back(L);
   };
-  const char* flat_env = getenv("HRT_GWALK_FLAT"); /* "0": instance chains stay whole leaf programs (A/B) */
+  const char* flat_env = knob_env("HRT_GWALK_FLAT"); /* "0": instance chains stay whole leaf programs (A/B) */
   const bool flat_ok = !(flat_env && strcmp(flat_env, "0") == 0);
-  const char* fl_env = getenv("HRT_GWALK_FLATLIST"); /* "0": a BvhNode leaf's Cuboid / List stays one program (A/B) */
+  const char* fl_env = knob_env("HRT_GWALK_FLATLIST"); /* "0": a BvhNode leaf's Cuboid / List stays one program (A/B) */
   const bool flat_lists = !(fl_env && strcmp(fl_env, "0") == 0);
   uint32_t i = 0;
   while (i < n) {
@@ -1396,7 +1396,7 @@ std::vector<WalkLeaf> gwalk_leaves(const hrt_scene* s, std::vector<WNode>* ref_t
  * it once, G19).  Such a box is kept as one leaf whose program is its whole subtree (trace_ray walks it
  * in the reference's order), which the leaf sequence is rebuilt with. */
 std::vector<WalkLeaf> gwalk_leaves_grouped(const hrt_scene* s, std::vector<WNode>* ref_tree, bool* regroup_ok) {
-  const char* ge = getenv("HRT_GWALK_GROUPED"); /* "0": no fallback (tests show the case it covers) */
+  const char* ge = knob_env("HRT_GWALK_GROUPED"); /* "0": no fallback (tests show the case it covers) */
   if (ge && strcmp(ge, "0") == 0) return gwalk_leaves(s, ref_tree, regroup_ok);
   std::vector<char> whole(s->g_nodes.size(), 0);
   for (;;) {
@@ -1427,15 +1427,14 @@ void build_walk(hrt_scene* s) {
   s->w_regroup_pending = false;
   s->w_general = false;
   if ((s->feature_mask & ~(G::F_BASIC | G::F_HEAVY_TEX)) != 0) { /* general scenes: the leaf-object stream */
-    const char* gw = getenv("HRT_GWALK"); /* "0": no general walk stream (segment kernels only) */
+    const char* gw = knob_env("HRT_GWALK"); /* "0": no general walk stream (segment kernels only) */
     if ((gw && strcmp(gw, "0") == 0) || s->media_nested) return;
     std::vector<WNode> T;
     bool regroup_ok = false;
     const std::vector<WalkLeaf> leaves = gwalk_leaves_grouped(s, &T, &regroup_ok);
     if (leaves.empty()) return;
     s->w_general = true;
-    const char* mode = getenv("HRT_WALK_TREE");
-    if (regroup_ok && !(mode && strcmp(mode, "reference") == 0)) {
+    if (regroup_ok && s->opts.walk_tree == 0) {
       const auto t0 = std::chrono::steady_clock::now();
       T.clear();
       walk_regroup(T, leaves);
@@ -1456,8 +1455,7 @@ void build_walk(hrt_scene* s) {
       bool gok = false;
       const std::vector<WalkLeaf> gl = gwalk_leaves_grouped(s, &TG, &gok);
       s->w_general = true;
-      const char* md = getenv("HRT_WALK_TREE");
-      if (gok && !(md && strcmp(md, "reference") == 0)) {
+      if (gok && s->opts.walk_tree == 0) {
         TG.clear();
         walk_regroup(TG, gl);
         s->w_regrouped = true;
@@ -1465,9 +1463,8 @@ void build_walk(hrt_scene* s) {
       walk_place_and_write(s, TG, gl);
       return;
     }
-  const char* mode = getenv("HRT_WALK_TREE");
-  const char* wb = getenv("HRT_WALK_BUILD"); /* host | device | auto (default) */
-  const bool regroup = regroup_ok && !(mode && strcmp(mode, "reference") == 0);
+  const char* wb = knob_env("HRT_WALK_BUILD"); /* host | device | auto (default) */
+  const bool regroup = regroup_ok && s->opts.walk_tree == 0;
   /* large scenes are re-grouped on the device at upload (build_walk.hip): until then the
    * stream keeps the reference hierarchy (valid for the host-side tools that read it) */
   if (regroup && (wb ? strcmp(wb, "device") == 0 : leaves.size() >= 32768)) s->w_regroup_pending = true;
@@ -1855,6 +1852,23 @@ hrt_status hrt_node_bounding_box(const hrt_scene* s, uint32_t node, float t0, fl
     *has_box = bbox(s, node, t0, t1, b) ? 1 : 0;
     if (*has_box)
       for (int a = 0; a < 3; a++) { bmin[a] = b.mn[a]; bmax[a] = b.mx[a]; }
+  });
+}
+
+hrt_status hrt_scene_set_options(hrt_scene* s, const hrt_scene_options* o) {
+  return guard([&] {
+    mutable_scene(s);
+    need(o != nullptr, HRT_ERR_INVALID_ARG, "hrt_scene_set_options: null options");
+    need(o->bvh_ties <= 1 && o->walk_tree <= 1 && o->chunk_uniform <= 1, HRT_ERR_INVALID_ARG,
+         "hrt_scene_set_options: bvh_ties, walk_tree and chunk_uniform are 0 or 1");
+    s->opts = *o;
+  });
+}
+
+hrt_status hrt_scene_get_options(const hrt_scene* s, hrt_scene_options* o) {
+  return guard([&] {
+    need(s && o, HRT_ERR_INVALID_ARG, "hrt_scene_get_options: null argument");
+    *o = s->opts;
   });
 }
 

@@ -86,6 +86,11 @@ struct WNode {
 };
 
 }  // namespace host
+
+/* knobs.cpp: the library's A/B environment knobs (none changes an image's bits).  Every read goes through
+ * knob_env; knobs_in_effect lists the set ones as "NAME=value;..." (hrt_last_launch). */
+const char* knob_env(const char* name);
+std::string knobs_in_effect();
 }  // namespace hrt
 
 struct hrt_scene {
@@ -99,6 +104,7 @@ struct hrt_scene {
   uint32_t bvh_tied_sorts = 0; /* BvhNode::new sorts of > 20 objects with equal keys (hrt_scene_info) */
   uint32_t n_media = 0;
   bool committed = false;
+  hrt_scene_options opts{}; /* explicit configuration (hrt_scene_set_options); all-zero = default */
 
   /* ---- flattened (valid after commit) ---- */
   std::vector<hrt::gpu::Node> g_nodes;
@@ -124,8 +130,8 @@ struct hrt_scene {
   bool w_device_built = false; /* ... by the device-side build (build_walk.hip) */
   bool w_regroup_pending = false; /* re-grouping left to the device build at upload */
   bool w_general = false;    /* the stream is the general-scene walk stream (layout.h; build_gwalk) */
-  uint32_t w_half = 16;
-  bool w_generic = true;     /* general stream: a leaf's program is neither GL_ONE nor GL_MED (needs trace_ray) */      /* bytes from a node part's first 16 B to its second (16, or layout.h WALK_SPLIT_HALF) */
+  uint32_t w_half = 16;      /* bytes from a node part's first 16 B to its second (16, or layout.h WALK_SPLIT_HALF) */
+  bool w_generic = true;     /* general stream: a leaf's program is neither GL_ONE nor GL_MED (needs trace_ray) */
   uint32_t w_build_us = 0;   /* time of the re-grouping (host or device) */
   size_t off_walk = 0;
   uint32_t feature_mask = 0;

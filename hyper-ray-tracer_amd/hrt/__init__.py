@@ -139,11 +139,17 @@ class LaunchInfo(ctypes.Structure):
     _fields_ = [("kernel", ctypes.c_char * 160)] + [
         (n, ctypes.c_uint32) for n in ("grid", "block", "blocks_per_cu", "cus", "waves_per_simd", "vgprs", "scratch_bytes",
                                        "lds_bytes")
-    ]
+    ] + [("knobs", ctypes.c_char * 256)]
+
+
+class SceneOptions(ctypes.Structure):
+    """hrt_scene_options: the explicit configuration that can change an image's bits (all-zero = default)."""
+    _fields_ = [(n, ctypes.c_uint32) for n in ("bvh_ties", "walk_tree", "chunk_min", "chunk_max", "chunk_uniform")]
 
 
 # Diagnostics an older build may lack; only tolerated when HRT_LIB points at another build (A/B runs)
-OPTIONAL = {"hrt_last_launch", "hrt_debug_box_test"}
+OPTIONAL = {"hrt_last_launch", "hrt_debug_box_test", "hrt_scene_set_options", "hrt_scene_get_options",
+            "hrt_debug_sample_chunks"}
 HRT_LIB_OVERRIDE = bool(os.environ.get("HRT_LIB"))
 
 # Every entry point of include/hrt/hrt.h (tests/test_abi.py checks the header against this list).
@@ -156,7 +162,8 @@ EXPORTS = [
     "hrt_node_bounding_box", "hrt_scene_set_root", "hrt_scene_commit", "hrt_preset_build", "hrt_camera_init",
     "hrt_render_tiles_device", "hrt_render_device", "hrt_render", "hrt_tile_grid", "hrt_scene_get_info", "hrt_last_launch", "hrt_debug_box_test",
     "hrt_debug_device_math", "hrt_debug_trace_path", "hrt_debug_scene_blob", "hrt_image_write", "hrt_render_progressive", "hrt_debug_prim_record",
-    "hrt_scene_synchronize", "hrt_debug_poke_blob",
+    "hrt_scene_synchronize", "hrt_debug_poke_blob", "hrt_scene_set_options", "hrt_scene_get_options",
+    "hrt_debug_sample_chunks",
 ]
 
 _lib = None
@@ -229,6 +236,9 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hrt_debug_trace_path": (S, [vp, ctypes.POINTER(Camera), ctypes.POINTER(RenderParams), u32, u32, u32, u32, vp, _U32P]),
         "hrt_scene_synchronize": (S, [vp]),
         "hrt_debug_poke_blob": (S, [vp, u64, vp, u64]),
+        "hrt_scene_set_options": (S, [vp, ctypes.POINTER(SceneOptions)]),
+        "hrt_scene_get_options": (S, [vp, ctypes.POINTER(SceneOptions)]),
+        "hrt_debug_sample_chunks": (S, [vp, ctypes.POINTER(RenderParams), _U32P]),
     }
     for name, (res, args) in sig.items():
         if name in OPTIONAL and HRT_LIB_OVERRIDE and not hasattr(L, name):
@@ -354,6 +364,21 @@ class Scene:
         _check(load().hrt_node_bounding_box(self.h, node, t0, t1, ctypes.byref(has), mn, mx))
         return (tuple(mn), tuple(mx)) if has.value else None
 
+    def set_options(self, **kw):
+        """hrt_scene_set_options: bvh_ties (0 stable / 1 reversed), walk_tree (0 re-grouped / 1 the reference tree),
+        chunk_min, chunk_max, chunk_uniform (sample chunks); unnamed fields keep their current values."""
+        o = self.options()
+        for k, v in kw.items():
+            if k not in dict(SceneOptions._fields_):
+                raise TypeError(f"unknown scene option {k!r}")
+            setattr(o, k, int(v))
+        _check(load().hrt_scene_set_options(self.h, ctypes.byref(o)))
+
+    def options(self) -> SceneOptions:
+        o = SceneOptions()
+        _check(load().hrt_scene_get_options(self.h, ctypes.byref(o)))
+        return o
+
     def set_root(self, node):
         _check(load().hrt_scene_set_root(self.h, node))
 
@@ -404,11 +429,14 @@ def load_image(path: str) -> np.ndarray:
     return np.ascontiguousarray(a[..., None] if a.ndim == 2 else a)
 
 
-def preset(name_or_id, scene_seed: int = 1, image: Optional[np.ndarray] = None) -> Scene:
-    """Build one of the reference scenes (application.rs:497-935) with a seeded builder stream."""
+def preset(name_or_id, scene_seed: int = 1, image: Optional[np.ndarray] = None, options: Optional[dict] = None) -> Scene:
+    """Build one of the reference scenes (application.rs:497-935) with a seeded builder stream; `options` are
+    hrt_scene_options fields, set before the builder runs (bvh_ties applies to its BvhNode::new calls)."""
     pid = PRESETS[name_or_id] if isinstance(name_or_id, str) else int(name_or_id)
     img = synthetic_earth() if image is None else np.ascontiguousarray(image, np.uint8)
     s = Scene()
+    if options:
+        s.set_options(**options)
     info = PresetInfo()
     h, w, c = img.shape
     _check(load().hrt_preset_build(s.h, pid, scene_seed, img.ctypes.data, w, h, c, ctypes.byref(info)))
@@ -471,12 +499,18 @@ def render_tiles_device(scene: Scene, cam: Camera, p: RenderParams, tiles, d_out
     return st if want_stats else None
 
 
-def last_launch() -> dict:
-    """The calling thread's last render launch (hrt_last_launch): kernel, grid, occupancy, VGPRs, scratch, LDS."""
+def last_launch() -> Optional[dict]:
+    """The calling thread's last render launch (hrt_last_launch): kernel, grid, occupancy, VGPRs, scratch, LDS, and
+    the library's A/B environment knobs set in this process.  None with an older build that lacks the entry
+    point (an A/B run through HRT_LIB)."""
+    L = load()
+    if not hasattr(L, "hrt_last_launch"):
+        return None
     li = LaunchInfo()
-    _check(load().hrt_last_launch(ctypes.byref(li)))
-    d = {n: getattr(li, n) for n, _ in LaunchInfo._fields_[1:]}
+    _check(L.hrt_last_launch(ctypes.byref(li)))
+    d = {n: getattr(li, n) for n, _ in LaunchInfo._fields_[1:-1]}
     d["kernel"] = li.kernel.decode()
+    d["knobs"] = li.knobs.decode()
     d["waves"] = li.grid * li.block // 64
     return d
 
@@ -564,6 +598,13 @@ def render_progressive(scene: "Scene", cam: Camera, p: RenderParams, on_tile, ti
     if err:
         raise err[0]
     return st if stats else None
+
+
+def sample_chunks(scene: "Scene", p: RenderParams) -> dict:
+    """hrt_debug_sample_chunks: the chunk schedule a render of `p` would sum each pixel's samples in."""
+    out = (ctypes.c_uint32 * 4)()
+    _check(load().hrt_debug_sample_chunks(scene.h, ctypes.byref(p), out))
+    return {"chunk": out[0], "head": out[1], "first": out[2], "tail": out[3]}
 
 
 def scene_blob(scene: "Scene"):

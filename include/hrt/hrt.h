@@ -205,6 +205,23 @@ hrt_status hrt_node_count(const hrt_scene* s, uint32_t node, uint32_t* count);
 hrt_status hrt_node_bounding_box(const hrt_scene* s, uint32_t node, float time0, float time1,
                                  int32_t* has_box, float box_min[3], float box_max[3]);
 
+/* Scene options: explicit configuration, as the reference takes its configuration as arguments
+ * (src/arguments.rs:23-47); the library reads nothing that can change an image from the environment.
+ * All-zero is the default.  Set before the nodes they affect (bvh_ties: hrt_node_bvh and the preset
+ * builders; everything else: hrt_scene_commit and the renders); after commit, HRT_ERR_STATE. */
+typedef struct hrt_scene_options {
+  uint32_t bvh_ties;       /* 0: BvhNode::new's equal sort keys in stable order; 1: each run of ties reversed
+                              (another order Rust's sort_unstable_by may produce, bvh_node.rs:34) */
+  uint32_t walk_tree;      /* 0: the walk's hierarchy re-grouped over the reference leaf order; 1: the reference
+                              BvhNode tree itself (same image bit for bit) */
+  uint32_t chunk_min;      /* sample chunks (a pixel's samples summed in chunks, then the chunk sums in chunk
+                              order): smallest chunk, 0 = the scene class's default */
+  uint32_t chunk_max;      /* at most this many head chunks, 0 = default */
+  uint32_t chunk_uniform;  /* 1: no halving tail chunks */
+} hrt_scene_options;
+hrt_status hrt_scene_set_options(hrt_scene* s, const hrt_scene_options* options);
+hrt_status hrt_scene_get_options(const hrt_scene* s, hrt_scene_options* options);
+
 hrt_status hrt_scene_set_root(hrt_scene* s, uint32_t node);
 /* Flatten + upload to HIP device `device` (-1: the calling thread's current device). */
 hrt_status hrt_scene_commit(hrt_scene* s, int32_t device);
@@ -295,6 +312,8 @@ typedef struct hrt_launch_info {
   uint32_t vgprs;          /* registers per lane */
   uint32_t scratch_bytes;  /* private (scratch) bytes per lane: register spills and stack */
   uint32_t lds_bytes;      /* dynamic LDS per workgroup */
+  char knobs[256];         /* the library's A/B environment knobs set in this process ("NAME=value;..."; empty:
+                              none).  None of them changes an image's bits (hrt_scene_options does that) */
 } hrt_launch_info;
 hrt_status hrt_last_launch(hrt_launch_info* out);
 /* Write an RGBA f32 frame (w x h, row-major, row 0 = image y 0 = bottom, as the render calls produce;
@@ -335,6 +354,11 @@ typedef struct hrt_blob_info {
                             * sphere streams staged whole in LDS (layout.h WALK_SPLIT_HALF) */
 } hrt_blob_info;
 hrt_status hrt_debug_scene_blob(hrt_scene* s, void* out, uint64_t cap, uint64_t* size, hrt_blob_info* info);
+/* The sample chunks a render of these params would use (no device involved; flattens an uncommitted scene):
+ * out[0] = chunk size, out[1] = head chunks, out[2] = samples of the first chunk, out[3] = halving tail chunks.
+ * A pixel's samples are summed chunk by chunk and the chunk sums added in chunk order, so this schedule is
+ * what fixes the image's bits beyond the paths themselves (hrt_scene_options chunk_*). */
+hrt_status hrt_debug_sample_chunks(hrt_scene* s, const hrt_render_params* p, uint32_t* out4);
 /* Overwrite n bytes of the committed scene's DEVICE blob at byte `offset` (hrt_blob_info offsets), after
  * a device synchronisation.  Fault injection for the watchdog test (e.g. a skip link pointing back). */
 hrt_status hrt_debug_poke_blob(hrt_scene* s, uint64_t offset, const void* data, uint64_t n);
@@ -345,7 +369,7 @@ hrt_status hrt_debug_prim_record(const hrt_scene* s, int32_t order, uint32_t ind
  * host/device bit identity. */
 hrt_status hrt_debug_device_math(int32_t op, const float* x, const float* y, float* out, uint32_t n);
 /* The walk's inflated box test (CULL_EXACT's culling half, lane.h box_ce; form 0: sub/mul/add, 1: the fused
- * o*inv form) on every (box, ray) pair, on the DEVICE (on_device = 1) or with the same code compiled for
+ * o*inv form) on every (box, ray) pair, on the DEVICE (on_device = 1: the calling thread's current HIP device) or with the same code compiled for
  * the host (0): boxes n_boxes x 8 floats (C.xyz, -, E.xyz, -), rays n_rays x 6 floats (origin, direction),
  * out[b * n_rays + q] = 1 if box b passes for ray q on [tmin, tmax].  Used by the GPU test that holds the
  * device's culling decisions to the host's bit for bit. */

@@ -7,6 +7,7 @@
 #     "smoke"                                    __graft_entry__.smoke()                        -> smoke.log
 #     "bench <tag> [bench args]"                 one bench.py line                              -> <tag>.jsonl
 #     "rehearsal <tag> [bench args]"             2 ranks sharing GPU 0 (--one-device)           -> <tag>.jsonl
+#     "rehtrace <tag> [bench args]"              the same under rocprofv3 --kernel-trace         -> prof_<tag>/
 #     "configs <tag>"                            BASELINE configs 3-5 lines (C4 / C5 also as an 8-way share)
 #     "profile <tag> <preset> <W> <H> <spp> [share] [bench args]"
 #                                                rocprofv3 kernel trace + PMC passes over one bench run,
@@ -77,11 +78,17 @@ step() {
       else run tests 900 python -u -m pytest tests -m gpu -x -v --durations=25 --timeout 200 --timeout-method thread -p no:cacheprovider; fi ;;
     smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) local tag=$1; shift; bench_line "$tag" 600 "$@" ;;
-    rehearsal)
+    rehearsal)  # bench.py starts its own ranks (hrt/launcher.py): no torchrun
       local tag=$1; shift
       echo "== $tag: 2-rank rehearsal $*" >> "$LOG"
-      timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-        --master-port 29533 bench.py --gpus 2 --one-device "$@" >> "$OUT/$tag.jsonl" 2>> "$OUT/$tag.err"
+      timeout -k 10 240 python -u bench.py --gpus 2 --one-device "$@" >> "$OUT/$tag.jsonl" 2>> "$OUT/$tag.err"
+      local rc=$?; echo "== $tag exit $rc" >> "$LOG"; return $rc ;;
+    rehtrace)  # kernel timeline of a concurrent 2-rank rehearsal (both ranks' launches on one GPU clock)
+      local tag=$1; shift
+      echo "== $tag: rocprofv3 kernel trace of a 2-rank rehearsal $*" >> "$LOG"
+      export TMPDIR=/tmp
+      timeout -k 10 300 rocprofv3 --kernel-trace -d "$OUT/prof_${tag}" -o run --output-format csv -- \
+        python3 "$ROOT/bench.py" --gpus 2 --one-device "$@" >> "$OUT/$tag.jsonl" 2>> "$OUT/$tag.err"
       local rc=$?; echo "== $tag exit $rc" >> "$LOG"; return $rc ;;
     configs)
       local tag=$1

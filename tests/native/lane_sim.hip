@@ -188,11 +188,9 @@ int lane_sim_render(const void* blob, const hrt_blob_info* bi, const hrt_camera*
   P.H = p->height;
   set_pixel_rcp(P);
   P.spp = p->samples;
-  P.chunk = sample_chunk(P.spp, chunk_class(bi->feature_mask, bi->main_end));
   {
-    const char* ct = getenv("HRT_CHUNK_TAIL");
-    uint32_t nh = 0, first = 0, nt = 0;
-    chunk_plan(P.spp, P.chunk, ct ? (uint32_t)atoi(ct) : 32u, nh, first, nt);
+    uint32_t nh = 0, first = 0, nt = 0; /* the default scene options (hrt_scene_options all zero) */
+    frame_chunks(P.spp, chunk_class(bi->feature_mask, bi->main_end), P.W, P.H, 0u, 0u, 32u, P.chunk, nh, first, nt);
     P.chunk_head = nh;
     P.chunk_first = first;
     P.n_chunks = nh + nt;

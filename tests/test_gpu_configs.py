@@ -183,9 +183,7 @@ def test_bvh_tie_order_sensitivity(name, W, H, spp, earth, monkeypatch):
 
     out = {}
     for mode in ("", "reverse"):
-        if mode:
-            monkeypatch.setenv("HRT_BVH_TIES", mode)
-        s = hrt.preset(name, 1, earth)
+        s = hrt.preset(name, 1, earth, options={"bvh_ties": 1 if mode else 0})
         _, info = hrt.scene_blob(s)
         s.commit()
         cam = hrt.preset_camera(s.info, W, H)

@@ -442,3 +442,28 @@ def test_final_walk_variants_are_bit_identical(earth, monkeypatch, knob):
     s2.commit()
     b, sb = hrt.render(s2, cam, p, stats=True)
     assert sa.segments == sb.segments and np.array_equal(a, b), knob
+    assert hrt.last_launch()["knobs"] == knob, hrt.last_launch()["knobs"]  # the launch reports the A/B knob
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,w,h,spp", [("random", 64, 36, 100), ("cornell", 48, 48, 150)])
+def test_env_chunk_knobs_do_not_change_frame(earth, monkeypatch, name, w, h, spp):
+    """the r04 environment knobs that regrouped each pixel's sum (HRT_CHUNK_MIN / DIV /
+    TAIL) are no longer read: with them set the default ABI renders the same bits and reports no knob.  The
+    explicit option (hrt_scene_options.chunk_min) does regroup the sums: same rays, a different summation
+    order (within the parity bar of the oracle, not bit-identical)."""
+    s = hrt.preset(name, 1, earth)
+    s.commit()
+    cam = hrt.preset_camera(s.info, w, h)
+    p = hrt.params(w, h, spp, 50, 9, tuple(s.info.background))
+    a, sa = hrt.render(s, cam, p, stats=True)
+    for k, v in (("HRT_CHUNK_MIN", "1"), ("HRT_CHUNK_DIV", "512"), ("HRT_CHUNK_TAIL", "0")):
+        monkeypatch.setenv(k, v)
+    b, sb = hrt.render(s, cam, p, stats=True)
+    assert sa.segments == sb.segments and np.array_equal(a, b)
+    assert hrt.last_launch()["knobs"] == ""
+    s2 = hrt.preset(name, 1, earth, options={"chunk_min": 1, "chunk_max": 512, "chunk_uniform": 1})
+    assert hrt.sample_chunks(s2, p) != hrt.sample_chunks(s, p)
+    s2.commit()
+    c, sc = hrt.render(s2, cam, p, stats=True)
+    assert sc.segments == sa.segments and float(np.abs(c - a).max()) <= 1e-5

@@ -144,7 +144,8 @@ def _c_layout(structs, tmp_path):
 
 PY_CLASSES = {"hrt_camera": "Camera", "hrt_render_params": "RenderParams", "hrt_tile": "Tile",
               "hrt_render_stats": "RenderStats", "hrt_tile_pixels": "TilePixels", "hrt_blob_info": "BlobInfo",
-              "hrt_preset_info": "PresetInfo", "hrt_scene_info": "SceneInfo", "hrt_launch_info": "LaunchInfo"}
+              "hrt_preset_info": "PresetInfo", "hrt_scene_info": "SceneInfo", "hrt_launch_info": "LaunchInfo",
+              "hrt_scene_options": "SceneOptions"}
 
 
 def test_struct_sizes_and_offsets_match_c(tmp_path):

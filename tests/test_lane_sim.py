@@ -58,8 +58,9 @@ def sim_submuladd(tmp_path_factory):
     return _build_sim(tmp_path_factory, ("-DHRT_BOX_FMA=0",))
 
 
-def sim_render(L, name, w, h, spp, depth, seed, earth, kernel, cull, region=None, sample_offset=0, t_min=0.001):
-    s = hrt.preset(name, 1, earth)
+def sim_render(L, name, w, h, spp, depth, seed, earth, kernel, cull, region=None, sample_offset=0, t_min=0.001,
+               options=None):
+    s = hrt.preset(name, 1, earth, options=options)
     blob, info = hrt.scene_blob(s)
     cam = hrt.preset_camera(s.info, w, h)
     p = hrt.params(w, h, spp, depth, seed, tuple(s.info.background), sample_offset=sample_offset, t_min=t_min)
@@ -180,13 +181,12 @@ def test_walk_stream_regrouped_equals_reference_hierarchy(sim, earth, name, monk
     """The sphere kernel's walk stream re-groups the inner boxes over the reference's leaf order
     (scene.cpp build_walk): bit-identical to the walk over the reference hierarchy, with fewer node visits."""
     a, sa = sim_render(sim, name, 48, 27, 4, 50, 5, earth, kernel=0, cull=CULL_EXACT)
-    monkeypatch.setenv("HRT_WALK_TREE", "reference")
-    b, sb = sim_render(sim, name, 48, 27, 4, 50, 5, earth, kernel=0, cull=CULL_EXACT)
+    b, sb = sim_render(sim, name, 48, 27, 4, 50, 5, earth, kernel=0, cull=CULL_EXACT, options={"walk_tree": 1})
     assert sa["segments"] == sb["segments"] and sa["prims"] == sb["prims"]
     assert np.array_equal(a, b)
-    _, info = hrt.scene_blob(hrt.preset(name, 1, earth))
+    _, info = hrt.scene_blob(hrt.preset(name, 1, earth, options={"walk_tree": 1}))
     assert info.walk_regrouped == 0 and info.walk_bytes > 0
-    monkeypatch.delenv("HRT_WALK_TREE")
+    monkeypatch.setenv("HRT_WALK_TREE", "reference")  # r04's environment knob: no longer read by the library
     _, info = hrt.scene_blob(hrt.preset(name, 1, earth))
     assert info.walk_regrouped == 1
     if name != "two_spheres":  # (two leaves: nothing to re-group)
@@ -214,8 +214,7 @@ def test_general_walk_lane_matches_oracle_and_general_lane(sim, earth, name, w, 
 @pytest.mark.parametrize("name", ["cornell", "final", "features", "cornell_smoke", "simple_light"])
 def test_general_walk_stream_regrouped_equals_reference_hierarchy(sim, earth, name, monkeypatch):
     a, sa = sim_render(sim, name, 32, 24, 4, 50, 5, earth, kernel=3, cull=CULL_EXACT)
-    monkeypatch.setenv("HRT_WALK_TREE", "reference")
-    b, sb = sim_render(sim, name, 32, 24, 4, 50, 5, earth, kernel=3, cull=CULL_EXACT)
+    b, sb = sim_render(sim, name, 32, 24, 4, 50, 5, earth, kernel=3, cull=CULL_EXACT, options={"walk_tree": 1})
     assert sa["segments"] == sb["segments"] and sa["prims"] == sb["prims"]
     assert np.array_equal(a, b)
     print(name, "node visits: re-grouped", sa["nodes"], "reference hierarchy", sb["nodes"])
