@@ -20,8 +20,8 @@ N fresh ranks before anything touches the GPU, forwards rank 0's line and exits 
   --scaling weak   replicas: every rank renders the whole frame with its own next spp samples per pixel.
 Rank 0 prints ONE JSON line (contract in the task statement), with
   parity       per-pixel L-inf of the timed frame against the CPU oracle on a band of rows spread over
-               the frame, at the frame's full spp, plus equality of the ray counts (the metric's own
-               "per-pixel Linf vs CPU ref");
+               the frame (one GPU's share, --share N: on 16-px tiles spread over the share), at the frame's
+               full spp, plus equality of the ray counts (the metric's own "per-pixel Linf vs CPU ref");
   roofline     the kernel's real bound, VALU instruction issue (PMC counts of this build from
                profiles/roofline_pmc.json over the live launch time), with the LDS / HBM figures beside it;
   cpu_baseline the CPU restatement of the reference path (oracle/) on the same rows, timed on this
@@ -231,6 +231,61 @@ def cpu_leg(args, frame_rays_per_sample):
                         f"cgroup cpu.max quota {quota if quota else 'none'})",
     }
     return cb, rows, img, c
+
+
+def cpu_leg_tiles(args, tiles, frame_rays_per_sample):
+    """cpu_leg for one GPU's share of a tile split (the C4 / C5 config lines): the oracle on 16-px tiles spread
+    evenly over the share at the frame's full spp (each tile's rows in 8-px tasks on the usable cores), as many
+    as the CPU budget allows (at least one).  Returns (cpu_baseline dict, picked tile indices, the oracle's
+    pixels of those tiles packed as the share is, oracle counters)."""
+    import numpy as np
+
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+
+    threads, quota = usable_cpus()
+    o = O.OracleScene(hrt.PRESETS[args.preset], 1, earth_image())
+    W, H = args.width, args.height
+
+    def tile_render(t, spp):
+        x, y, w, h = t
+        img, c = o.render_rows(W, H, spp, list(range(y, y + h)), args.depth, seed=args.seed, threads=threads, x0=x, w=w,
+                               task_w=8)
+        return img, c
+
+    probe = tiles[len(tiles) // 2]
+    t0 = time.perf_counter()
+    _, c = tile_render(probe, 4)
+    rate = c["segments"] / max(1e-6, time.perf_counter() - t0)
+    per_tile = c["segments"] / 4 * args.spp
+    n = max(1, min(len(tiles), int(args.cpu_seconds * rate / max(1.0, per_tile))))
+    picks = sorted({min(len(tiles) - 1, int((k + 0.5) * len(tiles) / n)) for k in range(n)})
+    t0 = time.perf_counter()
+    imgs, tot = [], {}
+    for i in picks:
+        img, c = tile_render(tiles[i], args.spp)
+        imgs.append(img.reshape(-1))
+        for k, v in c.items():
+            tot[k] = tot.get(k, 0) + v
+    dt = time.perf_counter() - t0
+    seg_per_sample = tot["segments"] / max(1, tot["samples"])
+    cb = {
+        "value": round(tot["segments"] / dt / 1e6, 4),
+        "unit": "Mrays/s",
+        "cores": threads,
+        "kind": "port",
+        "label": "CPU restatement of the reference path (oracle/, not the reference binary)",
+        "sample": f"{len(picks)} of the share's {len(tiles)} 16-px tiles, spread evenly, at {args.spp} spp "
+                  f"({tot['samples']} samples, {tot['segments']} rays, {dt:.1f} s); reference aabb.rs culling",
+        "segments_per_sample": round(seg_per_sample, 4),
+        "frame_segments_per_sample": round(frame_rays_per_sample, 4),
+        "sample_vs_frame": round(seg_per_sample / max(1e-9, frame_rays_per_sample), 4),
+        "host_cpu": host_cpu(),
+        "nproc": os.cpu_count(),
+        "cpu_quota": quota,
+        "threads_note": f"{threads} worker threads = the CPUs this job may use (cgroup cpu.max quota {quota if quota else 'none'})",
+    }
+    return cb, picks, np.concatenate(imgs), tot
 
 
 def pmc_key(args, share):
@@ -514,7 +569,27 @@ def main():
         frame = out.view(H, W, 4)
 
     cpu, parity = None, None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and share > 1 and not args.no_cpu_baseline:
+        # one GPU's share (C4 / C5 config lines): the oracle on tiles spread over the share, and the metric's
+        # L-inf on those tiles of the timed launch's packed output
+        cpu, picks, ref_px, cnt = cpu_leg_tiles(args, tiles, seg_step / max(1, samples_step))
+        if not args.no_parity:
+            import numpy as np
+
+            offs = np.cumsum([0] + [t[2] * t[3] for t in tiles])
+            packed = out.cpu().numpy()
+            got = np.concatenate([packed[4 * offs[i]:4 * offs[i + 1]] for i in picks])
+            sel = [tiles[i] for i in picks]
+            band_out = torch.empty(tiling.share_pixels(sel) * 4, dtype=torch.float32, device=dev)
+            band = hrt.render_tiles_device(scene, cam, p, sel, band_out.data_ptr(), stream.cuda_stream, want_stats=True)
+            band_same = bool((band_out.cpu().numpy() == got).all())
+            linf = float(abs(got - ref_px).max())
+            rays_equal = int(band.segments) == cnt["segments"]
+            parity = {"linf": linf, "tol": TOL, "pass": bool(linf <= TOL and rays_equal), "rays_equal": rays_equal,
+                      "gpu_rays": int(band.segments), "cpu_rays": cnt["segments"], "tiles": len(picks),
+                      "pixels": tiling.share_pixels(sel), "spp": args.spp, "band_render_equals_share_tiles": band_same,
+                      "reference": "oracle/ CPU restatement of the reference path, same seed and samples"}
+    elif rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, rows, ref_rows, cnt = cpu_leg(args, seg_step / max(1, samples_step))
         if not args.no_parity:
             got = out.view(H, W, 4)[torch.tensor(rows, device=dev)].cpu().numpy()

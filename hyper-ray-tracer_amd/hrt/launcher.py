@@ -113,4 +113,5 @@ def run_ranks(cmd: List[str], world: int, *, env: Optional[Dict[str, str]] = Non
             time.sleep(poll_s)
     finally:
         for sig, h in prev.items():
-            signal.signal(sig, h)
+            if h is not None:  # None: a handler installed outside Python (e.g. a profiler's), left as it is
+                signal.signal(sig, h)

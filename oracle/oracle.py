@@ -14,7 +14,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "liboracle.so")
+LIB = os.environ.get("ORACLE_LIB") or os.path.join(HERE, "liboracle.so")  # ORACLE_LIB: the ASan build (scripts/sanitize.sh)
 COUNTERS = ["segments", "aabb", "sphere", "moving", "rect", "medium", "tex_solid", "tex_checker", "tex_noise", "tex_image", "samples", "pixels"]
 
 _lib = None

@@ -87,15 +87,17 @@ step() {
       local tag=$1; shift
       echo "== $tag: rocprofv3 kernel trace of a 2-rank rehearsal $*" >> "$LOG"
       export TMPDIR=/tmp
-      timeout -k 10 300 rocprofv3 --kernel-trace -d "$OUT/prof_${tag}" -o run --output-format csv -- \
+      timeout -k 10 300 rocprofv3 --kernel-trace -d "$OUT/prof_${tag}" -o run_%pid% --output-format csv -- \
         python3 "$ROOT/bench.py" --gpus 2 --one-device "$@" >> "$OUT/$tag.jsonl" 2>> "$OUT/$tag.err"
       local rc=$?; echo "== $tag exit $rc" >> "$LOG"; return $rc ;;
     configs)
       local tag=$1
-      bench_line "${tag}_configs" 300 --steps 1 --warmup 1 --no-cpu-baseline --no-delivery --preset earth_perlin --spp 1000 && \
+      # C3 with its parity rows and CPU baseline; C4's whole frame without (one 4K row at 2000 spp is ~70 s of the
+      # oracle's reference culling); C4's and C5's 1/8 shares with parity tiles and a CPU baseline on tiles
+      bench_line "${tag}_configs" 300 --steps 1 --warmup 1 --no-delivery --preset earth_perlin --spp 1000 && \
       bench_line "${tag}_configs" 400 --steps 1 --warmup 1 --no-cpu-baseline --no-delivery --preset random_10k --width 3840 --height 2160 --spp 2000 && \
-      bench_line "${tag}_configs" 300 --steps 1 --warmup 1 --no-cpu-baseline --no-delivery --preset random_10k --width 3840 --height 2160 --spp 2000 --share 8 && \
-      bench_line "${tag}_configs" 300 --steps 1 --warmup 1 --no-cpu-baseline --no-delivery --preset cornell --width 2048 --height 2048 --spp 10000 --share 8 ;;
+      bench_line "${tag}_configs" 300 --steps 1 --warmup 1 --no-delivery --preset random_10k --width 3840 --height 2160 --spp 2000 --share 8 && \
+      bench_line "${tag}_configs" 300 --steps 1 --warmup 1 --no-delivery --preset cornell --width 2048 --height 2048 --spp 10000 --share 8 ;;
     profile) profile "$@" ;;
     probe) local tag=$1; shift; run "$tag" 600 python -u scripts/probe.py "$@" ;;
     libs)

@@ -5,6 +5,11 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# scripts/sanitize.sh preloads the clang ASan runtime into the test process itself; the compilers and helper
+# programs the tests start run without it (clang under a preloaded ASan runtime reports its own mmapped
+# sources as crashes)
+if "libclang_rt.asan" in os.environ.get("LD_PRELOAD", ""):
+    os.environ["HRT_SANITIZER_PRELOAD"] = os.environ.pop("LD_PRELOAD")
 sys.path.insert(0, os.path.join(ROOT, "hyper-ray-tracer_amd"))
 sys.path.insert(0, ROOT)
 

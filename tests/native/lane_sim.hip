@@ -11,8 +11,10 @@
  * tests/test_lane_sim.py checks it against the CPU oracle (oracle/) without a GPU.  It is built by the
  * tests (host-only compile) and is not part of libhrt.
  */
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <vector>
 
 #include "lane.h"
@@ -22,6 +24,139 @@ using namespace hrt;
 using namespace hrt::lane;
 
 namespace {
+
+/* ---- pricing a 4-wide walk, host only ----
+ * The sphere walk stream's binary hierarchy (re-grouped over the reference leaf order) collapsed one level:
+ * a wide record holds the boxes of a node's grandchildren (a leaf child is kept as it is), at most 4, in leaf
+ * order.  A lane visiting a record tests all its child boxes at once (the inflated test box_ce with its
+ * current closest) into a pass mask, then takes the passed children in order: a leaf gets its test right
+ * away (walk_leaf_test: the reference box test and the sphere against the current closest), an inner child is
+ * descended into with the rest of the mask kept on a per-level trail; a record whose mask runs out climbs
+ * to its parent (a dependent load of the parent's links).  Leaves are tested in the reference's order, each
+ * with the reference test, and every culled box holds its leaves, so the result must equal the binary walk's
+ * bit for bit (checked per segment).  Counted per segment: binary node steps and leaf tests; wide records,
+ * climbs, box tests, leaf tests; and per (8x8 block, sample, segment index) group the lockstep maxima. */
+struct WideTree {
+  struct N {
+    float4 a, b;
+    bool leaf;
+    uint32_t payload;
+    int kid[2];
+    int wk[4];
+    int nwk;
+  };
+  std::vector<N> T;
+  int root = -1;
+};
+struct WideStats {
+  uint64_t segs, bin_steps, bin_leaf, wide_records, wide_climbs, wide_tests, wide_leaf, mismatch;
+  uint64_t depth_max;
+};
+WideTree* g_wide = nullptr;
+int g_wide_arity = 4; /* 2: a record holds its node's two child boxes (no collapse) */
+WideStats g_ws;
+struct LockKey {
+  uint32_t block, sample, seg;
+  bool operator<(const LockKey& o) const {
+    return block != o.block ? block < o.block : (sample != o.sample ? sample < o.sample : seg < o.seg);
+  }
+};
+struct LockVal {
+  uint32_t bin_max, wide_max, n;
+  uint64_t bin_sum, wide_sum;
+};
+std::map<LockKey, LockVal>* g_lock = nullptr;
+std::map<uint64_t, uint32_t>* g_segidx = nullptr; /* (pixel, sample) -> segments so far */
+
+int wide_parse(const WalkSrc& src, uint32_t off, WideTree& W) {
+  const float4 a = wload<WM_HOST>(src, off), b = wload<WM_HOST>(src, off + src.half);
+  const int id = (int)W.T.size();
+  W.T.push_back(WideTree::N{a, b, false, 0u, {-1, -1}, {-1, -1, -1, -1}, 0});
+  const uint32_t pass = f2u(b.w);
+  if (walk_pending(pass)) {
+    W.T[id].leaf = true;
+    W.T[id].payload = pass - WALK_PEND;
+    return id;
+  }
+  const int c0 = wide_parse(src, pass, W);
+  const int c1 = wide_parse(src, f2u(W.T[c0].a.w), W); /* the first child's skip: its next sibling */
+  W.T[id].kid[0] = c0;
+  W.T[id].kid[1] = c1;
+  int n = 0;
+  for (int k : {c0, c1}) {
+    if (W.T[k].leaf || g_wide_arity == 2) W.T[id].wk[n++] = k;
+    else {
+      W.T[id].wk[n++] = W.T[k].kid[0];
+      W.T[id].wk[n++] = W.T[k].kid[1];
+    }
+  }
+  W.T[id].nwk = n;
+  return id;
+}
+
+void wide_price_segment(const KParams& P, const WalkSrc& src, const TRay& r, float bin_closest, uint32_t bin_winner,
+                        uint32_t bin_steps, uint32_t bin_leaf, uint32_t px, uint32_t py, uint32_t sample) {
+  const WideTree& W = *g_wide;
+  Counts cn{0u, 0u, 0u, 0u, 0u, 0u};
+  float closest = u2f(0x7f800000u);
+  uint32_t winner = G::NONE;
+  uint64_t records = 0, climbs = 0, tests = 0;
+  struct Lv {
+    int node;
+    uint32_t mask;
+  } st[96];
+  int depth = 0;
+  auto visit = [&](int n) {
+    records++;
+    uint32_t m = 0;
+    const WideTree::N& N = W.T[n];
+    for (int j = 0; j < N.nwk; j++) {
+      const WideTree::N& K = W.T[N.wk[j]];
+      tests++;
+      if (box_ce<HRT_BOX_FMA != 0, false>(K.a, K.b, r, P.t_min, closest)) m |= 1u << j;
+    }
+    st[depth++] = Lv{n, m};
+    if ((uint64_t)depth > g_ws.depth_max) g_ws.depth_max = depth;
+  };
+  const WideTree::N& R = W.T[W.root];
+  if (R.leaf) {
+    tests++;
+    if (box_ce<HRT_BOX_FMA != 0, false>(R.a, R.b, r, P.t_min, closest)) walk_leaf_test<true, WM_HOST>(P, src, R.payload, r, closest, winner, cn);
+  } else {
+    visit(W.root);
+    while (depth > 0) {
+      Lv& top = st[depth - 1];
+      if (top.mask == 0) {
+        depth--;
+        if (depth > 0) climbs++;
+        continue;
+      }
+      const int j = __builtin_ctz(top.mask);
+      top.mask &= top.mask - 1u;
+      const int k = W.T[top.node].wk[j];
+      if (W.T[k].leaf) walk_leaf_test<true, WM_HOST>(P, src, W.T[k].payload, r, closest, winner, cn);
+      else visit(k);
+    }
+  }
+  g_ws.segs++;
+  g_ws.bin_steps += bin_steps;
+  g_ws.bin_leaf += bin_leaf;
+  g_ws.wide_records += records;
+  g_ws.wide_climbs += climbs;
+  g_ws.wide_tests += tests;
+  g_ws.wide_leaf += cn.prims;
+  if (f2u(closest) != f2u(bin_closest) || winner != bin_winner) g_ws.mismatch++;
+  /* lockstep groups: the 64 lanes of an 8x8 block at one sample and one segment index */
+  const uint64_t key = ((uint64_t)(py * P.W + px) << 20) | sample;
+  const uint32_t seg = (*g_segidx)[key]++;
+  LockVal& v = (*g_lock)[LockKey{(py / 8u) * 4096u + px / 8u, sample, seg}];
+  const uint32_t wide_dep = (uint32_t)(records + climbs);
+  v.bin_max = std::max(v.bin_max, bin_steps);
+  v.wide_max = std::max(v.wide_max, wide_dep);
+  v.bin_sum += bin_steps;
+  v.wide_sum += wide_dep;
+  v.n++;
+}
 
 /* KIND 0: render_basic_kernel's lane, 1: render_full_kernel's lane, 2: render_kernel's (segment()),
  * 3: render_gwalk_kernel's (the general walk stream) */
@@ -90,7 +225,9 @@ void render_pixel(const KParams& P, uint32_t px, uint32_t py, float* rgba, uint6
             WalkSrc src;
             src.base = P.walk;
           src.half = P.walk_half;
+            const uint32_t nodes0 = cn.nodes, prims0 = cn.prims;
             while (node < P.walk_end) walk_step_host<true>(P, src, node, r, closest, winner, cn);
+            if (g_wide && node != G::NONE) wide_price_segment(P, src, r, closest, winner, cn.nodes - nodes0, cn.prims - prims0, px, py, sample);
           } else {
             while (node < P.main_end) basic_step<CULL, true>(P, P.nodes, P.prims, node, r, closest, winner, cn);
           }
@@ -226,6 +363,44 @@ int lane_sim_render(const void* blob, const hrt_blob_info* bi, const hrt_camera*
 }
 
 
+/* Price the 4-wide walk over the sphere scene's walk stream on a region (render_basic_kernel's lane, EXACT):
+ * renders the region as lane_sim_render (rgba, cnt), and for every segment walks the wide hierarchy too.
+ * out[0..11]: segments, binary node steps, binary leaf tests, wide records, wide climbs, wide box tests, wide
+ * leaf tests, segments whose wide result differs (must be 0), deepest trail, lockstep groups, sum over groups
+ * of 64 x the binary max steps, of 64 x the wide max dependent loads (records + climbs).  arity 2: records of
+ * the two child boxes of a node (no collapse), 4: of its grandchildren. */
+int lane_sim_wide_price(const void* blob, const hrt_blob_info* bi, const hrt_camera* cam, const hrt_render_params* p,
+                        uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, float* rgba, uint64_t* cnt, uint64_t* out,
+                        int arity) {
+  if (bi->walk_bytes == 0 || bi->walk_general || (arity != 2 && arity != 4)) return 1;
+  g_wide_arity = arity;
+  WideTree W;
+  WalkSrc src;
+  src.base = (const uint8_t*)blob + bi->off_walk;
+  src.half = bi->walk_half ? bi->walk_half : 16u;
+  W.root = wide_parse(src, 0u, W);
+  std::map<LockKey, LockVal> lock;
+  std::map<uint64_t, uint32_t> segidx;
+  g_wide = &W;
+  g_lock = &lock;
+  g_segidx = &segidx;
+  memset(&g_ws, 0, sizeof(g_ws));
+  const int rc = lane_sim_render(blob, bi, cam, p, 0, G::CULL_EXACT, x0, y0, w, h, rgba, cnt);
+  g_wide = nullptr;
+  g_lock = nullptr;
+  g_segidx = nullptr;
+  uint64_t groups = 0, bmax = 0, wmax = 0;
+  for (const auto& kv : lock) {
+    groups++;
+    bmax += 64ull * kv.second.bin_max;
+    wmax += 64ull * kv.second.wide_max;
+  }
+  const uint64_t v[12] = {g_ws.segs, g_ws.bin_steps, g_ws.bin_leaf, g_ws.wide_records, g_ws.wide_climbs, g_ws.wide_tests,
+                          g_ws.wide_leaf, g_ws.mismatch, g_ws.depth_max, groups, bmax, wmax};
+  memcpy(out, v, sizeof(v));
+  return rc;
+}
+
 /* The culling property behind CULL_EXACT on single spheres: whenever the reference's
  * sphere test (sphere.rs:38-55, lane.h sphere_root_at) accepts a root in [tmin, tmax], the walk's inflated
  * test (lane.h box_ce, both forms) on the sphere's box as the stream builder encodes it (walk_box.h
@@ -258,6 +433,38 @@ int lane_sim_cull_property(const float* sph, uint32_t n_sph, const float* rays, 
       if (p.x < mn[0] || p.x > mx[0] || p.y < mn[1] || p.y > mx[1] || p.z < mn[2] || p.z > mx[2]) cnt[1]++;
       if (!box_ce<true>(a, b, r, tmin, tmax)) cnt[2]++;
       if (!box_ce<false>(a, b, r, tmin, tmax)) cnt[3]++;
+    }
+  }
+  return 0;
+}
+
+/* the one-quadratic medium boundary (lane.h sphere_pair_at, what medium_pair / GL_MED leaves use)
+ * against the two boundary queries of constant_medium.rs:37-48 as the sphere test makes them
+ * (sphere_root_at over (-inf, inf), then over (t1 + 0.0001, inf)).  sph: n x (c, r); rays: m x (o, d).
+ * out[6 * (i * m + q) ..]: pair hits, t1, t2, two-call hits, t1, t2 (t = +inf where there is no hit). */
+int lane_sim_sphere_pair(const float* sph, uint32_t n_sph, const float* rays, uint32_t n_rays, float* out) {
+  const float inf = u2f(0x7f800000u);
+  for (uint32_t i = 0; i < n_sph; i++) {
+    const Vec3 c = v3(sph[4 * i], sph[4 * i + 1], sph[4 * i + 2]);
+    const float rad = sph[4 * i + 3];
+    for (uint32_t q = 0; q < n_rays; q++) {
+      const Vec3 o = v3(rays[6 * q], rays[6 * q + 1], rays[6 * q + 2]), d = v3(rays[6 * q + 3], rays[6 * q + 4], rays[6 * q + 5]);
+      float* w = out + 6 * ((size_t)i * n_rays + q);
+      float p1 = inf, p2 = inf;
+      w[0] = (float)sphere_pair_at(c, rad, o, d, p1, p2);
+      w[1] = p1;
+      w[2] = p2;
+      TRay r;
+      set_dir(r, o, d);
+      float t1 = inf, t2 = inf;
+      int hits = 0;
+      if (sphere_root_at(c, rad, r, -inf, inf, t1)) {
+        hits = 1;
+        if (sphere_root_at(c, rad, r, t1 + 0.0001f, inf, t2)) hits = 2;
+      }
+      w[3] = (float)hits;
+      w[4] = hits > 0 ? t1 : inf;
+      w[5] = hits > 1 ? t2 : inf;
     }
   }
   return 0;

@@ -245,11 +245,11 @@ def test_trimmed_general_kernel_equals_all_feature_kernel(name, w, h, spp, earth
     assert np.array_equal(a, b)
 
 
-def _share_exact_vs_reference(name, W, H, spp, share, earth, every=1):
-    """rank 0's share (or the whole frame, share 1) on the default EXACT path and on the verbatim reference
+def _share_exact_vs_reference(name, W, H, spp, share, earth, every=1, rank=0, start=0):
+    """rank `rank`'s share (or the whole frame, share 1) on the default EXACT path and on the verbatim reference
     traversal (HRT_RENDER_REFERENCE_CULL: aabb.rs's per-axis test alone, the segment kernel over the
     reference node stream): np.array_equal and equal world.hit counts.  every > 1: every every-th tile of
-    the share, rendered as one launch of the share's kind."""
+    the share from `start`, rendered as one launch of the share's kind."""
     import torch
 
     from hrt import tiling
@@ -258,7 +258,7 @@ def _share_exact_vs_reference(name, W, H, spp, share, earth, every=1):
     s.commit()
     cam = hrt.preset_camera(s.info, W, H)
     bg = tuple(s.info.background)
-    tiles = [(0, 0, W, H)] if share == 1 else tiling.split_tiles(W, H, share, 0)[::every]
+    tiles = [(0, 0, W, H)] if share == 1 else tiling.split_tiles(W, H, share, rank)[start::every]
     n = tiling.share_pixels(tiles)
     out = []
     for flags in (0, hrt.RENDER_REFERENCE_CULL):
@@ -267,7 +267,7 @@ def _share_exact_vs_reference(name, W, H, spp, share, earth, every=1):
                                      want_stats=True)
         out.append((d.cpu().numpy(), int(st.segments), hrt.last_launch()["kernel"]))
     (a, ra, ka), (b, rb, kb) = out
-    print(f"{name} {W}x{H} {spp} spp share 1/{share}: rays {ra} vs {rb}; {ka} vs {kb}")
+    print(f"{name} {W}x{H} {spp} spp rank {rank} of {share} ({len(tiles)} tiles): rays {ra} vs {rb}; {ka} vs {kb}")
     assert ra == rb
     assert np.array_equal(a, b)
     assert np.isfinite(a).all()
@@ -297,3 +297,68 @@ def test_c5_share8_exact_equals_reference_traversal(earth):
     equal to the reference traversal (the share where r03's earlier box form diverged in five paths)."""
     k = _share_exact_vs_reference("cornell", 2048, 2048, 10000, 8, earth)
     assert "launch_g" in k and "TRIM = 7" in k  # no media, no heavy textures, one-node programs only
+
+
+# VERDICT r04 item 3: every rank's share of the scaling configs, not rank 0's alone.  A seeded sample of each
+# rank's 16-px tiles (every 16th from a seeded start: 1/128 of the frame per rank, 1/16 over the 8 ranks)
+# on the default path against the verbatim reference traversal, bit for bit.
+_RANK_START = {r: (r * 7 + 3) % 16 for r in range(8)}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rank", range(8))
+def test_c4_every_rank_share_sample_exact_equals_reference_traversal(rank, earth):
+    k = _share_exact_vs_reference("random_10k", 3840, 2160, 2000, 8, earth, every=16, rank=rank, start=_RANK_START[rank])
+    assert "HYB = true" in k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rank", range(8))
+def test_c5_every_rank_share_sample_exact_equals_reference_traversal(rank, earth):
+    k = _share_exact_vs_reference("cornell", 2048, 2048, 10000, 8, earth, every=16, rank=rank, start=_RANK_START[rank])
+    assert "launch_g" in k
+
+
+def _share_tiles_vs_oracle(name, W, H, spp, rank, near, earth):
+    """The 16-px tiles of rank `rank`'s 1/8 share nearest the points `near`, rendered as ONE launch of those
+    tiles (the share's kind of call: packed tiles, the frame's chunk schedule), against the oracle's recursive
+    reference walk."""
+    import torch
+
+    from hrt import tiling
+
+    share = tiling.split_tiles(W, H, 8, rank)
+    tiles = [min(share, key=lambda t: (t[0] + 8 - x) ** 2 + (t[1] + 8 - y) ** 2) for x, y in near]
+    s = hrt.preset(name, 1, earth)
+    s.commit()
+    cam = hrt.preset_camera(s.info, W, H)
+    p = hrt.params(W, H, spp, 50, 1, tuple(s.info.background))
+    n = tiling.share_pixels(tiles)
+    d = torch.empty(n * 4, dtype=torch.float32, device="cuda")
+    st = hrt.render_tiles_device(s, cam, p, tiles, d.data_ptr(), 0, want_stats=True)
+    got = d.cpu().numpy()
+    o = O.OracleScene(hrt.PRESETS[name], 1, earth)
+    parts, segs = [], 0
+    for x, y, w, h in tiles:  # each tile's rows in 8-px tasks: the whole thread pool on one 16-px tile
+        img, cnt = o.render_rows(W, H, spp, list(range(y, y + h)), 50, seed=1, threads=THREADS, x0=x, w=w, task_w=8)
+        parts.append(img.reshape(-1))
+        segs += cnt["segments"]
+    ref = np.concatenate(parts)
+    linf = float(np.abs(got - ref).max())
+    print(f"{name} rank {rank} tiles {tiles}: rays {st.segments} vs {segs}, L-inf {linf:.3e}")
+    assert int(st.segments) == segs
+    assert linf <= TOL, linf
+
+
+@pytest.mark.gpu
+def test_c4_rank5_share_tiles_vs_oracle(earth):
+    """C4 (10k spheres, 3840x2160, 2000 spp): a 512-px band of rank 5's share (two of its 16-px tiles: the
+    sphere field near the horizon and the checker ground in front) against the oracle at full spp."""
+    _share_tiles_vs_oracle("random_10k", 3840, 2160, 2000, 5, [(1900, 700), (2500, 1150)], earth)
+
+
+@pytest.mark.gpu
+def test_c5_rank3_share_tile_vs_oracle(earth):
+    """C5 (Cornell 2048^2, 10000 spp): a 256-px tile of rank 3's share (inside the room) against the oracle
+    at full spp."""
+    _share_tiles_vs_oracle("cornell", 2048, 2048, 10000, 3, [(1300, 700)], earth)

@@ -36,7 +36,8 @@ def _build_sim(tmp_path_factory, extra=()):
     so = str(tmp_path_factory.mktemp("lanesim") / "liblanesim.so")
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     subprocess.run([hipcc, "-O2", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared",
-                    "--offload-host-only", *extra, "-I" + os.path.join(ROOT, "include"),
+                    "--offload-host-only", *extra, *os.environ.get("LANE_SIM_CFLAGS", "").split(),  # scripts/sanitize.sh
+                    "-I" + os.path.join(ROOT, "include"),
                     "-I" + os.path.join(ROOT, "hyper-ray-tracer_amd", "csrc"),
                     os.path.join(HERE, "native", "lane_sim.hip"), "-o", so], check=True)
     L = ctypes.CDLL(so)
@@ -323,6 +324,43 @@ def test_exact_culling_property_on_grazing_rays(sim):
     print("cull property totals", total)
     assert accepted > 100000 and outside > 0  # grazing false hits were produced and none was culled
     assert raised >= 60 and nan_rays > 0
+
+
+def test_medium_sphere_pair_equals_two_boundary_queries(sim):
+    """a medium over one sphere answers constant_medium.rs:37-48's two boundary queries
+    (boundary.hit(-inf, inf), then boundary.hit(t1 + 0.0001, inf)) from ONE evaluation of the quadratic
+    (lane.h sphere_pair_at, GL_MED leaves and medium_pair).  Held bit for bit to the two sphere tests made
+    separately (sphere_root_at) on grazing rays, origins inside, on and outside the sphere, rays starting
+    just past the near root, tangent rays, zero and denormal directions and NaN rays."""
+    rng = np.random.default_rng(13)
+    spheres = [(0.0, 0.0, 0.0, 5000.0), (0.0, 150.0, 145.0, 70.0), (360.0, 150.0, 145.0, 70.0), (4.0, 1.0, 0.0, 1.0),
+               (0.0, -1000.0, 0.0, 1000.0)]
+    spheres += [(*rng.uniform(-100, 100, 3), 10.0 ** rng.uniform(-2, 2)) for _ in range(20)]
+    fn = sim.lane_sim_sphere_pair
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+    total = np.zeros(3, np.int64)
+    for s in spheres:
+        c, rad = np.array(s[:3], np.float64), float(s[3])
+        rays = list(_cull_rays(rng, c, rad, 3000))  # grazing and missing rays around the sphere
+        for _ in range(600):  # origins inside, on and near the surface, random directions
+            d = rng.normal(size=3)
+            d /= np.linalg.norm(d)
+            o = c + d * rad * rng.choice([0.0, 0.3, 0.999, 1.0, 1.001, 2.0])
+            rays.append(np.r_[o, rng.normal(size=3) * 10.0 ** rng.uniform(-3, 3)])
+        o = c + np.array([rad * 2, 0.0, 0.0])
+        rays += [np.r_[o, -1.0, 0.0, 0.0], np.r_[o, 0.0, 0.0, 0.0], np.r_[o, 1e-42, 0.0, 0.0],
+                 np.r_[c + np.array([-rad * 2, rad, 0.0]), 1.0, 0.0, 0.0],  # tangent
+                 np.r_[o, np.nan, 0.0, 1.0], np.r_[np.nan, 0.0, 0.0, 1.0, 0.0, 0.0]]
+        rays = np.asarray(rays, np.float32)
+        sph = np.array(s, np.float32)
+        out = np.zeros((len(rays), 6), np.float32)
+        assert fn(sph.ctypes.data, 1, rays.ctypes.data, len(rays), out.ctypes.data) == 0
+        pair, two = out[:, :3], out[:, 3:]
+        assert np.array_equal(pair.view(np.uint32), two.view(np.uint32)), s  # bit for bit, NaN payloads included
+        for k in range(3):
+            total[k] += int((pair[:, 0] == k).sum())
+    print("sphere pair: rays with 0 / 1 / 2 boundary hits", total)
+    assert total.min() > 100  # every outcome was exercised
 
 
 def sim_render_scene(L, s, w, h, spp, kernel, cull, seed=11):
