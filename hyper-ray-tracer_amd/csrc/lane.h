@@ -88,6 +88,8 @@ struct KParams {
   uint32_t n_perlin;   /* Perlin tables (7 KB each); perlin_lds: the kernel stages them in LDS */
   uint32_t perlin_lds;
   uint32_t walk_half;  /* the walk stream's node-part split (layout.h WALK_SPLIT_HALF) or 16 */
+  uint32_t walk_c16;   /* 16-B node parts (layout.h WALK_C16): walk_end is then the node count */
+  uint32_t walk_pbase; /* walk_c16: byte offset of the payloads */
 };
 
 /* Sample-chunk size: spp <= cmin keeps one work item per pixel (the reference's sequential sum), larger
@@ -343,6 +345,38 @@ HRT_LANE_FI void wload_node(const WalkSrc& src, uint32_t off, float4& a, float4&
   b = wload<MEM>(src, off + (MEM == WM_HOST ? src.half : HALF));
 }
 
+
+/* ---- 16-B node parts (layout.h WALK_C16) ----
+ * One 16-B read per node step instead of two (LDS, or under the exec mask of the lanes whose part lies beyond
+ * the staged set in a hybrid stream); the box's six binary16 values are widened exactly to f32, so box_ce sees
+ * the encoded box's own numbers; the links are 16-bit node indices. */
+HRT_LANE_FI float h2f(uint32_t bits16) { return (float)__builtin_bit_cast(_Float16, (uint16_t)bits16); }
+template <int MEM>
+HRT_LANE_FI float4 wload_part16(const WalkSrc& src, uint32_t off) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (MEM == WM_HYB) { /* as wload_node: an LDS read for every lane, a buffer read for the global lanes */
+    const bool in_lds = off < src.hot;
+    const float4 l = wload<WM_LDS>(src, in_lds ? off : 0u);
+    float4 g = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (!in_lds) g = wload<WM_BUF>(src, off);
+    return in_lds ? l : g;
+  }
+#endif
+  return wload<MEM>(src, off);
+}
+/* a walk position of a 16-B stream parked on a leaf (WALK_C16_LEAF | payload index) */
+HRT_LANE_FI bool walk_pending16(uint32_t i) { return (i >> 15) == 1u; }
+template <bool C16>
+HRT_LANE_FI bool walk_pend(uint32_t i) {
+  if constexpr (C16) return walk_pending16(i);
+  return i - G::WALK_PEND < 0x7FFFFFFFu;
+}
+/* the payload offset of the leaf a lane is parked on */
+template <bool C16>
+HRT_LANE_FI uint32_t pend_payload(const KParams& P, uint32_t i) {
+  if constexpr (C16) return P.walk_pbase + (i & G::WALK_C16_MAX) * G::WALK_PAYLOAD_BYTES;
+  return i - G::WALK_PEND;
+}
 
 /* aabb.rs:20-47 (CULL_REFERENCE), its narrowed form (CULL_SLAB), or CULL_EXACT: the reference test
  * AND an inflated slab test that only rejects boxes no accepted hit can come from (layout.h).
@@ -1455,8 +1489,21 @@ HRT_LANE_FI bool box_ce(const float4& a, const float4& b, const TRay& r, float t
 /* FMA: box_ce's fused form (default except for the latency-bound hybrid walk; the sphere kernel's
  * HEAVY instantiation passes false: at its 128-VGPR cap the three more live registers cost 3% on C3) */
 template <bool COUNT, int MEM, bool FMA = HRT_BOX_FMA && (MEM != WM_HYB || HRT_BOX_FMA_ALL), bool NANG = true,
-          uint32_t HALF = 16>
+          uint32_t HALF = 16, bool C16 = false>
 HRT_LANE_FI void walk_box(const WalkSrc& src, uint32_t& i, const TRay& r, float tmin, float closest, Counts& cn) {
+  if constexpr (C16) { /* layout.h WALK_C16: position = node index, part at 16 i */
+    const float4 q = wload_part16<MEM>(src, i << 4);
+    const uint32_t w0 = f2u(q.x), w1 = f2u(q.y), w2 = f2u(q.z);
+    uint32_t links = f2u(q.w);
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm("" : "+v"(links));
+#endif
+    const float4 a = make_float4(h2f(w0 & 0xFFFFu), h2f(w0 >> 16), h2f(w1 & 0xFFFFu), 0.0f);
+    const float4 b = make_float4(h2f(w1 >> 16), h2f(w2 & 0xFFFFu), h2f(w2 >> 16), 0.0f);
+    if constexpr (COUNT) cn.nodes++;
+    i = box_ce<FMA, NANG>(a, b, r, tmin, closest) ? links >> 16 : links & 0xFFFFu;
+    return;
+  }
   float4 a, b;
   wload_node<MEM, HALF>(src, i, a, b);
   uint32_t skip = f2u(a.w);
@@ -1498,10 +1545,10 @@ HRT_LANE_FI void walk_leaf_test(const KParams& P, const WalkSrc& src, uint32_t l
 template <int MEM>
 HRT_LANE_FI uint32_t walk_successor(const WalkSrc& src, uint32_t leaf) { return f2u(wload<payload_mem<MEM>()>(src, leaf).w) >> 2; }
 
-template <bool COUNT, int MEM>
+template <bool COUNT, int MEM, bool C16 = false>
 HRT_LANE_FI void walk_prim(const KParams& P, const WalkSrc& src, uint32_t& i, const TRay& r, float& closest,
                            uint32_t& winner, Counts& cn) {
-  const uint32_t leaf = i - WALK_PEND; /* the leaf's payload */
+  const uint32_t leaf = pend_payload<C16>(P, i); /* the leaf's payload */
   i = walk_successor<MEM>(src, leaf); /* the walk goes on at the leaf's pre-order successor */
   walk_leaf_test<COUNT, MEM>(P, src, leaf, r, closest, winner, cn);
 }
@@ -1659,11 +1706,11 @@ HRT_LANE_FI void gwalk_prim(const KParams& P, const G::Node* __restrict__ nodes,
 }
 
 /* both halves back to back (the host lane simulator's walk) */
-template <bool COUNT>
+template <bool COUNT, bool C16 = false>
 HRT_LANE_FI void walk_step_host(const KParams& P, const WalkSrc& src, uint32_t& i, const TRay& r, float& closest,
                                 uint32_t& winner, Counts& cn) {
-  walk_box<COUNT, WM_HOST>(src, i, r, P.t_min, closest, cn);
-  if (walk_pending(i)) walk_prim<COUNT, WM_HOST>(P, src, i, r, closest, winner, cn);
+  walk_box<COUNT, WM_HOST, HRT_BOX_FMA != 0, true, 16u, C16>(src, i, r, P.t_min, closest, cn);
+  if (walk_pend<C16>(i)) walk_prim<COUNT, WM_HOST, C16>(P, src, i, r, closest, winner, cn);
 }
 
 /* The BASIC kernel (sphere scenes: the Random family), with POSTPONED shading.  A lane's walk state

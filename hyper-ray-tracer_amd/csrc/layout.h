@@ -217,6 +217,16 @@ constexpr uint32_t WALK_NODE_BYTES = 32, WALK_PAYLOAD_BYTES = 96;
  * no faster on C2 (14 024 vs 14 038 Mrays/s, profiles/r04g_ab.txt), so the conflicts are not what
  * bounds the step. */
 constexpr uint32_t WALK_SPLIT_HALF = 16384;
+/* 16-B node parts (r05, WALK_C16; hybrid sphere streams, the C4 class): the staged budget holds twice the node
+ * parts.  A part is four u32: (C.x | C.y << 16), (C.z | E.x << 16), (E.y | E.z << 16), (skip | pass << 16), C and
+ * E in IEEE binary16 (C rounded to nearest, E rounded up after adding C's rounding error, so the part's box
+ * holds the 32-B part's box and with it the node's geometry: all the inflated test needs), the links 16-bit
+ * node indices: node k's part at byte 16 k, the end = the node count N; pass of a leaf = WALK_C16_LEAF | j, its
+ * payload at walk_pbase + j * WALK_PAYLOAD_BYTES (payload records unchanged, their successor field a node
+ * index).  Walk positions are node indices; a lane parked on leaf j holds WALK_C16_LEAF | j.  Scenes with more
+ * than WALK_C16_MAX nodes or leaves, or coordinates beyond binary16's range, keep the 32-B parts
+ * (scene.cpp walk_transcode_c16). */
+constexpr uint32_t WALK_C16_MAX = 0x7FFFu, WALK_C16_LEAF = 0x8000u;
 constexpr uint32_t WL_MOVING = 1u, WL_NOBOX = 2u;
 enum : uint32_t { WT_SOLID = 0, WT_CHECKER = 1, WT_GLOBAL = 2 }; /* inline texture of a leaf's material */
 

@@ -604,7 +604,9 @@ KParams scene_params(const hrt_scene* s, const hrt_camera* cam, const hrt_render
   kp.motion_span = s->motion_span;
   kp.walk = base + s->off_walk;
   kp.walk_bytes = s->w_end;
-  kp.walk_end = s->w_end;
+  kp.walk_end = s->w_c16 ? s->w_nodes : s->w_end; /* layout.h WALK_C16: positions are node indices */
+  kp.walk_c16 = s->w_c16 ? 1u : 0u;
+  kp.walk_pbase = s->w_pbase;
   kp.walk_hot = (pl.gwalk && pl.gwalk_mem == WM_HYB) || (pl.lds && !pl.full && !pl.fast && pl.cull == G::CULL_EXACT)
                     ? s->w_hot : 0;
   kp.walk_half = s->w_half;

@@ -26,7 +26,8 @@ constexpr int sphere_waves() { return HEAVY ? HRT_HEAVY_WAVES : BASIC_WAVES; }
 /* HYB (CULL_EXACT with LDS): the walk stream exceeds the LDS budget; its first P.walk_hot bytes (the
  * hierarchy's top levels) are staged, the rest is read through the buffer descriptor (layout.h) */
 /* SPLIT: the stream's node parts are split (layout.h WALK_SPLIT_HALF; LDS, not HYB) */
-template <int CULL, bool COUNT, bool LDS, bool HYB = false, bool HEAVY = false, bool SPLIT = false>
+/* C16: 16-B node parts (layout.h WALK_C16; hybrid streams): walk positions are node indices */
+template <int CULL, bool COUNT, bool LDS, bool HYB = false, bool HEAVY = false, bool SPLIT = false, bool C16 = false>
 __global__ __launch_bounds__((basic_block_threads<LDS, sphere_waves<HEAVY>()>()), sphere_waves<HEAVY>())
 void render_basic_kernel(KParams P) {
   extern __shared__ float4 lds_scene[];
@@ -156,18 +157,18 @@ void render_basic_kernel(KParams P) {
         if constexpr (COUNT) cn.walk_slots++;
         if (node < end) {
           if constexpr (WS) walk_box<COUNT, WMEM, HRT_BOX_FMA && ((WMEM != WM_HYB && !HEAVY) || HRT_BOX_FMA_ALL), false,
-                                    SPLIT ? G::WALK_SPLIT_HALF : 16u>(ws, node, r, tmin_c, closest, cn); /* no rects: no NaN hits (lane.h set_noinv) */
+                                    SPLIT ? G::WALK_SPLIT_HALF : 16u, C16>(ws, node, r, tmin_c, closest, cn); /* no rects: no NaN hits (lane.h set_noinv) */
           else basic_box<CULL, COUNT, STRIDE>(P, nodes, node, r, closest, cn);
         } else if constexpr (COUNT) {
-          if (walk_pending(node)) cn.park_slots++;
+          if (walk_pend<C16>(node)) cn.park_slots++;
           else if (walking) cn.wait_slots++;
         }
         if ((u + 1) % PRIM_EVERY != 0) continue;
         if constexpr (SPEC) {
           /* a lane parked on a leaf with no test pending makes the leaf's test pending and walks on behind
            * it; a lane parks for good (blocked) only on a second leaf, or at the end of its walk */
-          if (walk_pending(node) && pend == G::NONE) {
-            pend = node - WALK_PEND;
+          if (walk_pend<C16>(node) && pend == G::NONE) {
+            pend = pend_payload<C16>(P, node);
             node = walk_successor<WMEM>(ws, pend);
           }
           const bool waiting = pend != G::NONE && !(node < end);
@@ -178,8 +179,8 @@ void render_basic_kernel(KParams P) {
             if (pend != G::NONE) { /* the pending tests of every lane, walking or blocked, in walk order */
               walk_leaf_test<COUNT, WMEM>(P, ws, pend, r, closest, winner, cn);
               pend = G::NONE;
-              if (walk_pending(node)) { /* blocked: its leaf's test becomes the pending one */
-                pend = node - WALK_PEND;
+              if (walk_pend<C16>(node)) { /* blocked: its leaf's test becomes the pending one */
+                pend = pend_payload<C16>(P, node);
                 node = walk_successor<WMEM>(ws, pend);
               }
             }
@@ -187,17 +188,17 @@ void render_basic_kernel(KParams P) {
           }
           continue;
         }
-        const bool waiting = walk_pending(node);
+        const bool waiting = walk_pend<C16>(node);
         const unsigned long long pm = __ballot(waiting);
         if (pm && ((uint32_t)__popcll(pm) >= batch || !__ballot(node < end))) {
           if constexpr (COUNT) cn.prim_slots++;
           if (waiting) {
-            if constexpr (WS) walk_prim<COUNT, WMEM>(P, ws, node, r, closest, winner, cn);
+            if constexpr (WS) walk_prim<COUNT, WMEM, C16>(P, ws, node, r, closest, winner, cn);
             else basic_prim<CULL, COUNT, STRIDE>(P, nodes, prims, node, r, closest, winner, cn);
           }
         }
       }
-      const unsigned long long live = __ballot(node < end || walk_pending(node) || (SPEC && pend != G::NONE));
+      const unsigned long long live = __ballot(node < end || walk_pend<C16>(node) || (SPEC && pend != G::NONE));
       if (!live || (uint32_t)__popcll(walkers & ~live) >= need) break;
       if (++iters > cap) { stuck = true; break; }
     }
@@ -211,7 +212,7 @@ void render_basic_kernel(KParams P) {
     }
     stamp(1);
     /* shade the finished segments (application.rs:483-494) */
-    const bool shading = walking && node >= end && !walk_pending(node) && (!SPEC || pend == G::NONE);
+    const bool shading = walking && node >= end && !walk_pend<C16>(node) && (!SPEC || pend == G::NONE);
     const bool traced = shading && node != G::NONE;
     bool sample_done = false, chunk_done = false;
     if (shading) {
@@ -260,9 +261,9 @@ void render_basic_kernel(KParams P) {
 }
 
 
-template <int CULL, bool COUNT, bool LDS, bool HYB = false, bool HEAVY = false, bool SPLIT = false>
+template <int CULL, bool COUNT, bool LDS, bool HYB = false, bool HEAVY = false, bool SPLIT = false, bool C16 = false>
 void launch_basic(const KParams& kp, int device, hipStream_t stream, size_t smem) {
-  const void* fn = (const void*)render_basic_kernel<CULL, COUNT, LDS, HYB, HEAVY, SPLIT>;
+  const void* fn = (const void*)render_basic_kernel<CULL, COUNT, LDS, HYB, HEAVY, SPLIT, C16>;
   const int block = basic_block_threads<LDS, sphere_waves<HEAVY>()>();
   /* LDS: the staged scene, then one u32 result slot per thread (layout.h LDS_SCENE_MAX_BYTES leaves
    * room for both, twice per CU) */
@@ -270,7 +271,7 @@ void launch_basic(const KParams& kp, int device, hipStream_t stream, size_t smem
   p.lane_lds = LDS ? (uint32_t)((smem + 15) & ~(size_t)15) : 0u;
   const size_t total = p.lane_lds + (size_t)block * sizeof(uint32_t);
   const int grid = resident_grid(fn, block, device, total, true, __PRETTY_FUNCTION__);
-  hipLaunchKernelGGL((render_basic_kernel<CULL, COUNT, LDS, HYB, HEAVY, SPLIT>), dim3(grid), dim3(block), total, stream, p);
+  hipLaunchKernelGGL((render_basic_kernel<CULL, COUNT, LDS, HYB, HEAVY, SPLIT, C16>), dim3(grid), dim3(block), total, stream, p);
   hip_check(hipGetLastError(), "render_basic_kernel launch");
 }
 
@@ -293,7 +294,12 @@ void launch_sphere(int cull, bool count, bool lds, bool heavy, const KParams& kp
              : launch_basic<G::CULL_EXACT, false, false, false, true>(kp, device, stream, 0);
     return;
   }
-  if (cull == G::CULL_EXACT && lds && kp.walk_hot > 0) { /* top levels in LDS, the rest in global memory */
+  if (cull == G::CULL_EXACT && kp.walk_c16) { /* 16-B node parts (layout.h WALK_C16: hybrid streams only) */
+    if (lds) count ? launch_basic<G::CULL_EXACT, true, true, true, false, false, true>(kp, device, stream, smem)
+                   : launch_basic<G::CULL_EXACT, false, true, true, false, false, true>(kp, device, stream, smem);
+    else count ? launch_basic<G::CULL_EXACT, true, false, false, false, false, true>(kp, device, stream, 0)
+               : launch_basic<G::CULL_EXACT, false, false, false, false, false, true>(kp, device, stream, 0);
+  } else if (cull == G::CULL_EXACT && lds && kp.walk_hot > 0) { /* top levels in LDS, the rest in global memory */
     if (count) launch_basic<G::CULL_EXACT, true, true, true>(kp, device, stream, smem);
     else launch_basic<G::CULL_EXACT, false, true, true>(kp, device, stream, smem);
   } else if (cull == G::CULL_EXACT && kp.walk_half != 16u) { /* split node parts (layout.h; F_BASIC scenes) */

@@ -12,6 +12,7 @@
  *   counts           hittable/.rs count() (Rotation::count == 1, rotation.rs:140-142)
  */
 #include <algorithm>
+#include <functional>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -811,12 +812,171 @@ void flatten(hrt_scene* s) {
 
 
 namespace hrt {
-/* The records (layout.h): every node part at addr[i], every leaf's payload at paddr[i].  Placement:
- * if the stream fits the LDS budget, pre-order with each payload right after its leaf (the whole
- * stream is staged in LDS); otherwise the node parts likeliest to be reached (largest parent box
- * surface first, up to the LDS budget) come first and are staged in LDS, the other node parts follow in
- * pre-order in global memory, then the payloads (w_hot = the staged bytes). */
-void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::vector<WalkLeaf>& leaves) {
+/* ---- 16-B node parts (layout.h WALK_C16) ----
+ * IEEE binary16 of a finite double: round to nearest even (up = false) or towards +inf (up = true, x >= 0).
+ * Returns false when the value does not fit (|x| > 65504 after rounding). */
+static bool half_round(double x, bool up, uint16_t& bits, double& value) {
+  const double ax = fabs(x);
+  if (!(ax <= 65504.0)) return false;
+  if (ax == 0.0) {
+    bits = std::signbit(x) ? 0x8000u : 0u;
+    value = 0.0;
+    return true;
+  }
+  int e = (int)floor(log2(ax));
+  if (ldexp(1.0, e) > ax) e--; /* log2 rounding */
+  if (ldexp(1.0, e + 1) <= ax) e++;
+  if (e < -14) e = -14; /* subnormals share the smallest exponent's ulp */
+  const double ulp = ldexp(1.0, e - 10);
+  double q = ax / ulp; /* exact: a power-of-two scaling */
+  q = up ? (x >= 0 ? ceil(q) : floor(q)) : nearbyint(q);
+  double v = q * ulp;
+  if (!(v <= 65504.0)) return false;
+  /* bits of the exactly representable v */
+  uint32_t b;
+  if (v < ldexp(1.0, -14)) b = (uint32_t)(v / ldexp(1.0, -24)); /* subnormal */
+  else {
+    int ve = (int)floor(log2(v));
+    if (ldexp(1.0, ve) > v) ve--;
+    if (ldexp(1.0, ve + 1) <= v) ve++;
+    const uint32_t mant = (uint32_t)(v / ldexp(1.0, ve - 10)) - 1024u;
+    b = (uint32_t)(ve + 15) << 10 | mant;
+  }
+  bits = (uint16_t)(b | (x < 0 ? 0x8000u : 0u));
+  value = x < 0 ? -v : v;
+  return true;
+}
+
+/* Transcode a finished hybrid sphere stream (32-B node parts densely in [0, 32 N), the payloads behind them)
+ * into 16-B node parts (layout.h WALK_C16): per node (C, E) as binary16 -- C rounded to nearest, E rounded UP,
+ * so [C' - E', C' + E'] holds the 32-B part's box [C - E, C + E] and therefore the node's geometry, which is
+ * all the inflated test needs (any boxes holding their leaves), with CE_FLOOR kept on the
+ * rounded values.  Children first: an inner node's encoded box also holds its children's ENCODED boxes, so
+ * inclusion stays monotone as in the 32-B stream (every hierarchy over the same leaves then culls the same
+ * leaves).  The links become 16-bit node indices (pass of a leaf: WALK_C16_LEAF | its payload index); the
+ * payloads move down by 16 N bytes and their successor fields become node indices.  Left as it is when a scene
+ * does not fit the format (more than WALK_C16_MAX nodes or leaves, coordinates beyond binary16's range). */
+void walk_transcode_c16(hrt_scene* s, uint32_t N) {
+  const uint32_t END = s->w_end, NB = 32u * N, PB = G::WALK_PAYLOAD_BYTES;
+  if (N == 0 || N > G::WALK_C16_MAX || END < NB || (END - NB) % PB != 0 || (END - NB) / PB > G::WALK_C16_MAX) return;
+  const std::vector<float>& o = s->w_stream;
+  auto unit = [&](uint32_t off) -> uint32_t { return off == END ? N : off / 32u; };
+  std::vector<uint32_t> packed((size_t)N * 4);
+  std::vector<double> lo((size_t)N * 3), hi((size_t)N * 3); /* each node's encoded box */
+  std::vector<char> done(N, 0), inf_box(N, 0);
+  bool ok = true;
+  /* post-order from the root (node 0): children = pass, and the first child's skip */
+  std::function<void(uint32_t, int)> enc = [&](uint32_t j, int depth) {
+    if (!ok) return;
+    if (j >= N || done[j] || depth > 200) {
+      ok = false;
+      return;
+    }
+    const float* a = &o[(size_t)j * 8];
+    const float* b = a + 4;
+    const uint32_t skip = f2u(a[3]), pass = f2u(b[3]);
+    double L[3], H[3];
+    bool inf = false;
+    for (int k = 0; k < 3; k++) {
+      if (b[k] == HUGE_VALF) inf = true;
+      L[k] = (double)a[k] - (double)b[k];
+      H[k] = (double)a[k] + (double)b[k];
+    }
+    uint32_t pu;
+    if (pass & G::WALK_PEND) {
+      const uint32_t q = pass & ~G::WALK_PEND;
+      if (q < NB || (q - NB) % PB != 0) {
+        ok = false;
+        return;
+      }
+      pu = G::WALK_C16_LEAF | (q - NB) / PB;
+    } else {
+      if (pass >= NB || pass % 32u != 0) {
+        ok = false;
+        return;
+      }
+      const uint32_t c0 = pass / 32u;
+      enc(c0, depth + 1);
+      if (!ok) return;
+      const uint32_t s0 = f2u(o[(size_t)c0 * 8 + 3]);
+      if (s0 >= NB || s0 % 32u != 0) {
+        ok = false;
+        return;
+      }
+      const uint32_t c1 = s0 / 32u;
+      enc(c1, depth + 1);
+      if (!ok) return;
+      for (uint32_t c : {c0, c1}) {
+        inf = inf || inf_box[c];
+        for (int k = 0; k < 3; k++) {
+          L[k] = std::min(L[k], lo[(size_t)c * 3 + k]);
+          H[k] = std::max(H[k], hi[(size_t)c * 3 + k]);
+        }
+      }
+      pu = c0;
+    }
+    if (skip != END && (skip >= NB || skip % 32u != 0)) {
+      ok = false;
+      return;
+    }
+    uint16_t hc[3] = {0, 0, 0}, he[3] = {0x7C00u, 0x7C00u, 0x7C00u}; /* a box-less leaf: C = 0, E = +inf */
+    double cv[3] = {0, 0, 0}, ev[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL};
+    if (!inf) {
+      double cmax = 0.0, emax = 0.0;
+      for (int k = 0; k < 3; k++) {
+        if (!half_round(0.5 * (L[k] + H[k]), false, hc[k], cv[k]) ||
+            !half_round(std::max(cv[k] - L[k], H[k] - cv[k]), true, he[k], ev[k])) {
+          ok = false;
+          return;
+        }
+        cmax = std::max(cmax, fabs(cv[k]));
+        emax = std::max(emax, ev[k]);
+      }
+      if (emax < ldexp(cmax, -12)) /* CE_FLOOR on the encoded box (walk_box.h) */
+        for (int k = 0; k < 3; k++)
+          if (ev[k] < ldexp(cmax, -12) && !half_round(ldexp(cmax, -12), true, he[k], ev[k])) {
+            ok = false;
+            return;
+          }
+    }
+    for (int k = 0; k < 3; k++) {
+      lo[(size_t)j * 3 + k] = cv[k] - ev[k];
+      hi[(size_t)j * 3 + k] = cv[k] + ev[k];
+    }
+    inf_box[j] = inf;
+    done[j] = 1;
+    packed[(size_t)j * 4 + 0] = (uint32_t)hc[0] | (uint32_t)hc[1] << 16;
+    packed[(size_t)j * 4 + 1] = (uint32_t)hc[2] | (uint32_t)he[0] << 16;
+    packed[(size_t)j * 4 + 2] = (uint32_t)he[1] | (uint32_t)he[2] << 16;
+    packed[(size_t)j * 4 + 3] = unit(skip) | pu << 16;
+  };
+  enc(0u, 0);
+  for (uint32_t j = 0; ok && j < N; j++) ok = done[j] != 0; /* every node part reached from the root */
+  if (!ok) return;
+  const uint32_t n_leaf = (END - NB) / PB, pbase = 16u * N;
+  std::vector<float> t((size_t)(pbase + n_leaf * PB) / 4, 0.0f);
+  for (size_t k = 0; k < packed.size(); k++) t[k] = u2f(packed[k]);
+  for (uint32_t l = 0; l < n_leaf; l++) {
+    const float* src = &o[(size_t)(NB + l * PB) / 4];
+    float* dst = &t[(size_t)(pbase + l * PB) / 4];
+    std::copy(src, src + PB / 4, dst);
+    const uint32_t w = f2u(dst[3]); /* flags | successor << 2 */
+    const uint32_t succ = w >> 2;
+    if (succ != END && (succ >= NB || succ % 32u != 0)) return;
+    dst[3] = u2f((w & 3u) | unit(succ) << 2);
+  }
+  s->w_stream.swap(t);
+  s->w_end = pbase + n_leaf * PB;
+  s->w_hot /= 2; /* the staged node parts at half the bytes */
+  s->w_c16 = true;
+  s->w_pbase = pbase;
+}
+
+/* c16: a hybrid sphere stream is laid out for 16-B node parts: twice the node parts selected for the staged
+ * set, then transcoded (walk_transcode_c16).  Returns false when that was asked for and could not be done
+ * (the caller lays the stream out again without it). */
+static bool walk_place_and_write_impl(hrt_scene* s, const std::vector<WNode>& T, const std::vector<WalkLeaf>& leaves,
+                                      bool c16) {
   const uint32_t N = (uint32_t)T.size();
   uint64_t total = 0;
   const uint32_t PB = s->w_general ? G::GWALK_PAYLOAD_BYTES : G::WALK_PAYLOAD_BYTES;
@@ -830,6 +990,12 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
   const uint32_t budget = s->w_general && !(big_env && strcmp(big_env, "0") == 0) ? G::GWALK_LDS_BIG_BYTES
                                                                                    : G::LDS_SCENE_MAX_BYTES;
   const bool hybrid = total > G::LDS_SCENE_MAX_BYTES && !(hot_env && strcmp(hot_env, "0") == 0);
+  const char* pl = knob_env("HRT_WALK_PAYLOADS");
+  const bool apart = !(pl && strcmp(pl, "inline") == 0);
+  /* 16-B parts: the F_BASIC sphere kernel only (textured sphere scenes keep the 32-B parts of its HEAVY walk) */
+  c16 = c16 && hybrid && apart && !s->w_general && !s->w_regroup_pending && N <= G::WALK_C16_MAX &&
+        (s->feature_mask & ~G::F_BASIC) == 0;
+  const uint32_t stage_budget = c16 ? 2u * budget : budget; /* in 32-B parts: halved by the transcode */
   uint32_t off = 0;
   std::vector<char> hot(N, 0);
   /* Hybrid placement (C4 1/8 share, r03u: +1.5% for both together, bit-identical): the node parts staged
@@ -837,9 +1003,7 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
    * top levels breadth first), and the global node parts stay dense in pre-order with every payload
    * after them (HRT_WALK_PAYLOADS=inline: each payload behind its leaf) */
   const char* hotsel = knob_env("HRT_WALK_HOTSEL");
-  const char* pl = knob_env("HRT_WALK_PAYLOADS");
   const bool by_area = !(hotsel && strcmp(hotsel, "depth") == 0);
-  const bool apart = !(pl && strcmp(pl, "inline") == 0);
   if (hybrid) {
     std::vector<uint32_t> order(N);
     for (uint32_t i = 0; i < N; i++) order[i] = i;
@@ -859,7 +1023,7 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
       std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return T[a].depth < T[b].depth; });
     }
     for (uint32_t i : order) {
-      if (off + G::WALK_NODE_BYTES > budget) break;
+      if (off + G::WALK_NODE_BYTES > stage_budget) break;
       addr[i] = off;
       off += G::WALK_NODE_BYTES;
       hot[i] = 1;
@@ -1027,6 +1191,17 @@ void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::
     put4(o, q + 80, Bc[0], Bc[1], Bc[2], u2f(m.kind | wt << 4 | mi << 8));
   }
   s->w_end = END;
+  s->w_nodes = N;
+  s->w_c16 = false;
+  s->w_pbase = 0;
+  if (c16) walk_transcode_c16(s, N);
+  return !c16 || s->w_c16;
+}
+
+void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::vector<WalkLeaf>& leaves) {
+  const char* c16_env = knob_env("HRT_WALK_C16"); /* "0": keep the 32-B node parts (A/B) */
+  const bool c16 = !(c16_env && strcmp(c16_env, "0") == 0);
+  if (!walk_place_and_write_impl(s, T, leaves, c16)) walk_place_and_write_impl(s, T, leaves, false);
 }
 
 /* The leaf sequence of the reference stream (its pre-order) and the reference hierarchy over it. */
@@ -1948,6 +2123,9 @@ hrt_status hrt_debug_scene_blob(hrt_scene* s, void* out, uint64_t cap, uint64_t*
       info->box_t1 = s->box_t1;
       info->off_walk = s->off_walk;
       info->walk_bytes = s->w_end;
+      info->walk_c16 = s->w_c16 ? 1u : 0u;
+      info->walk_nodes = s->w_nodes;
+      info->walk_pbase = s->w_pbase;
       info->walk_regrouped = s->w_regrouped ? 1u : 0u;
       info->bvh_tied_sorts = s->bvh_tied_sorts;
       info->walk_hot = s->w_hot;

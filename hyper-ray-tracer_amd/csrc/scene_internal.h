@@ -131,6 +131,9 @@ struct hrt_scene {
   bool w_regroup_pending = false; /* re-grouping left to the device build at upload */
   bool w_general = false;    /* the stream is the general-scene walk stream (layout.h; build_gwalk) */
   uint32_t w_half = 16;      /* bytes from a node part's first 16 B to its second (16, or layout.h WALK_SPLIT_HALF) */
+  uint32_t w_nodes = 0;      /* node parts of the stream */
+  bool w_c16 = false;        /* 16-B node parts (layout.h WALK_C16; hybrid sphere streams) */
+  uint32_t w_pbase = 0;      /* w_c16: byte offset of the payloads (payload j at w_pbase + j * WALK_PAYLOAD_BYTES) */
   bool w_generic = true;     /* general stream: a leaf's program is neither GL_ONE nor GL_MED (needs trace_ray) */
   uint32_t w_build_us = 0;   /* time of the re-grouping (host or device) */
   size_t off_walk = 0;
@@ -179,6 +182,7 @@ std::vector<uint8_t> build_blob(hrt_scene* s); /* scene.cpp: the arrays in one b
  * and the placement + records of a hierarchy over them */
 std::vector<host::WalkLeaf> walk_leaves(const hrt_scene* s, std::vector<host::WNode>* ref_tree, bool* regroup_ok);
 void walk_place_and_write(hrt_scene* s, const std::vector<host::WNode>& T, const std::vector<host::WalkLeaf>& leaves);
+void walk_transcode_c16(hrt_scene* s, uint32_t N);
 /* scene.cpp: the general-scene walk stream's leaf objects (layout.h) in the reference's pre-order; a
  * BvhNode box whose reference-stream index is marked in `whole` stays ONE leaf (its subtree the program),
  * and gwalk_leaves_grouped marks every box whose group's box-less leaves would not be contiguous */

@@ -109,7 +109,8 @@ class BlobInfo(ctypes.Structure):
          ("off_walk", ctypes.c_uint64), ("walk_bytes", ctypes.c_uint32), ("walk_regrouped", ctypes.c_uint32),
          ("bvh_tied_sorts", ctypes.c_uint32), ("walk_hot", ctypes.c_uint32),
                 ("walk_general", ctypes.c_uint32), ("off_chains", ctypes.c_uint64),
-        ("walk_half", ctypes.c_uint32)]
+        ("walk_half", ctypes.c_uint32), ("walk_c16", ctypes.c_uint32), ("walk_nodes", ctypes.c_uint32),
+        ("walk_pbase", ctypes.c_uint32)]
 
 
 class PresetInfo(ctypes.Structure):

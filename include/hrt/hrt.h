@@ -352,6 +352,10 @@ typedef struct hrt_blob_info {
   uint64_t off_chains;     /* every instance's transform chain, outermost first (layout.h CHAIN_F4) */
   uint32_t walk_half;      /* bytes from a walk-stream node part's first 16 B to its second: 16, or the split of
                             * sphere streams staged whole in LDS (layout.h WALK_SPLIT_HALF) */
+  uint32_t walk_c16;       /* 1: 16-B node parts (layout.h WALK_C16; hybrid sphere streams): positions are node
+                            * indices, the walk ends at walk_nodes, payloads from walk_pbase */
+  uint32_t walk_nodes;     /* node parts of the walk stream */
+  uint32_t walk_pbase;     /* walk_c16: byte offset of the payloads */
 } hrt_blob_info;
 hrt_status hrt_debug_scene_blob(hrt_scene* s, void* out, uint64_t cap, uint64_t* size, hrt_blob_info* info);
 /* The sample chunks a render of these params would use (no device involved; flattens an uncommitted scene):

@@ -37,11 +37,11 @@ def price(L, preset, W, H, spp, rows, x0=0, w=None, seed=1, arity=4):
     cam = hrt.preset_camera(s.info, W, H)
     p = hrt.params(W, H, spp, 50, seed, tuple(s.info.background))
     w = W - x0 if w is None else w
-    tot = np.zeros(12, np.uint64)
+    tot = np.zeros(16, np.uint64)
     for y in rows:  # 8-row bands: whole 8x8 blocks, the lockstep groups of the kernels' waves
         out = np.zeros((8, w, 4), np.float32)
         cnt = np.zeros(8, np.uint64)
-        o = np.zeros(12, np.uint64)
+        o = np.zeros(16, np.uint64)
         rc = L.lane_sim_wide_price(blob, ctypes.byref(info), ctypes.byref(cam), ctypes.byref(p), x0, y, w, 8,
                                    out.ctypes.data_as(ctypes.c_void_p), cnt.ctypes.data_as(ctypes.c_void_p),
                                    o.ctypes.data_as(ctypes.c_void_p), arity)
@@ -51,7 +51,8 @@ def price(L, preset, W, H, spp, rows, x0=0, w=None, seed=1, arity=4):
         tot[9:] += o[9:]
     seg = int(tot[0])
     r = {k: int(v) for k, v in zip(["segments", "bin_steps", "bin_leaf", "wide_records", "wide_climbs", "wide_tests",
-                                     "wide_leaf", "mismatch", "depth_max", "groups", "bin_lock", "wide_lock"], tot)}
+                                     "wide_leaf", "mismatch", "depth_max", "groups", "bin_lock", "wide_lock",
+                                     "lock_steps", "lock_cold_77k32", "lock_cold_77k16", "lock_cold_152k32"], tot)}
     per = {k: round(r[k] / seg, 3) for k in ("bin_steps", "bin_leaf", "wide_records", "wide_climbs", "wide_tests", "wide_leaf")}
     per["wide_dependent"] = round((r["wide_records"] + r["wide_climbs"]) / seg, 3)
     per["bin_lane_util"] = round(r["bin_steps"] / max(1, r["bin_lock"]), 3)
@@ -60,6 +61,8 @@ def price(L, preset, W, H, spp, rows, x0=0, w=None, seed=1, arity=4):
     # VALU under lockstep: a binary iteration ~28 VALU (23 for the node step + loop control); a wide iteration
     # runs the record visit (4 box tests ~76 + mask / trail ~10; arity 2: 2 tests ~38 + 6) and the climb (~8)
     # for every lane of the wave
+    for k in ("lock_cold_77k32", "lock_cold_77k16", "lock_cold_152k32"):  # lockstep steps a wave waits on global memory
+        per[k + "_share"] = round(r[k] / max(1, r["lock_steps"]), 4)
     per["valu_lock_ratio_wide_over_bin"] = round(r["wide_lock"] * (94 if arity == 4 else 52) / max(1, r["bin_lock"] * 28), 3)
     return r, per
 

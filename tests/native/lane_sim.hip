@@ -44,13 +44,21 @@ struct WideTree {
     int kid[2];
     int wk[4];
     int nwk;
+    double key; /* the builder's staging priority: the parent box's half area (scene.cpp walk_place_and_write) */
+    int depth;
   };
   std::vector<N> T;
   int root = -1;
+  /* hot[b][n]: node n staged in LDS under staging budget b (HOT_BUDGETS node parts) */
+  std::vector<std::vector<char>> hot;
 };
+/* staged node parts: 77 KB of 32-B parts (today's sphere kernel), of 16-B parts (a compressed format in the
+ * same LDS), 152 KB of 32-B parts (one 1024-thread workgroup per CU) */
+constexpr uint32_t HOT_BUDGETS[3] = {77u * 1024u / 32u, 77u * 1024u / 16u, 152u * 1024u / 32u};
 struct WideStats {
   uint64_t segs, bin_steps, bin_leaf, wide_records, wide_climbs, wide_tests, wide_leaf, mismatch;
   uint64_t depth_max;
+  uint64_t lock_steps, lock_global[3]; /* lockstep binary steps; those where some lane reads a non-staged part */
 };
 WideTree* g_wide = nullptr;
 int g_wide_arity = 4; /* 2: a record holds its node's two child boxes (no collapse) */
@@ -64,22 +72,24 @@ struct LockKey {
 struct LockVal {
   uint32_t bin_max, wide_max, n;
   uint64_t bin_sum, wide_sum;
+  std::vector<uint8_t> global; /* per binary step index: bit b set when some lane's node is cold under budget b */
 };
 std::map<LockKey, LockVal>* g_lock = nullptr;
 std::map<uint64_t, uint32_t>* g_segidx = nullptr; /* (pixel, sample) -> segments so far */
 
-int wide_parse(const WalkSrc& src, uint32_t off, WideTree& W) {
+int wide_parse(const WalkSrc& src, uint32_t off, WideTree& W, double key = 1e300, int depth = 0) {
   const float4 a = wload<WM_HOST>(src, off), b = wload<WM_HOST>(src, off + src.half);
   const int id = (int)W.T.size();
-  W.T.push_back(WideTree::N{a, b, false, 0u, {-1, -1}, {-1, -1, -1, -1}, 0});
+  W.T.push_back(WideTree::N{a, b, false, 0u, {-1, -1}, {-1, -1, -1, -1}, 0, key, depth});
   const uint32_t pass = f2u(b.w);
   if (walk_pending(pass)) {
     W.T[id].leaf = true;
     W.T[id].payload = pass - WALK_PEND;
     return id;
   }
-  const int c0 = wide_parse(src, pass, W);
-  const int c1 = wide_parse(src, f2u(W.T[c0].a.w), W); /* the first child's skip: its next sibling */
+  const double ha = 4.0 * ((double)b.x * b.y + (double)b.y * b.z + (double)b.z * b.x); /* half area of [C - E, C + E] */
+  const int c0 = wide_parse(src, pass, W, ha, depth + 1);
+  const int c1 = wide_parse(src, f2u(W.T[c0].a.w), W, ha, depth + 1); /* the first child's skip: its next sibling */
   W.T[id].kid[0] = c0;
   W.T[id].kid[1] = c1;
   int n = 0;
@@ -92,6 +102,22 @@ int wide_parse(const WalkSrc& src, uint32_t off, WideTree& W) {
   }
   W.T[id].nwk = n;
   return id;
+}
+
+/* the binary walk again over the parsed tree (the kernel's walk without speculation: the same node
+ * sequence as walk_step_host), recording the nodes it visits */
+void bin_walk_nodes(const KParams& P, const WalkSrc& src, const TRay& r, int n, float& closest, uint32_t& winner,
+                    std::vector<int>& seq) {
+  const WideTree& W = *g_wide;
+  Counts cn{0u, 0u, 0u, 0u, 0u, 0u};
+  seq.push_back(n);
+  if (!box_ce<HRT_BOX_FMA != 0, false>(W.T[n].a, W.T[n].b, r, P.t_min, closest)) return;
+  if (W.T[n].leaf) {
+    walk_leaf_test<true, WM_HOST>(P, src, W.T[n].payload, r, closest, winner, cn);
+    return;
+  }
+  bin_walk_nodes(P, src, r, W.T[n].kid[0], closest, winner, seq);
+  bin_walk_nodes(P, src, r, W.T[n].kid[1], closest, winner, seq);
 }
 
 void wide_price_segment(const KParams& P, const WalkSrc& src, const TRay& r, float bin_closest, uint32_t bin_winner,
@@ -151,6 +177,17 @@ void wide_price_segment(const KParams& P, const WalkSrc& src, const TRay& r, flo
   const uint32_t seg = (*g_segidx)[key]++;
   LockVal& v = (*g_lock)[LockKey{(py / 8u) * 4096u + px / 8u, sample, seg}];
   const uint32_t wide_dep = (uint32_t)(records + climbs);
+  {
+    std::vector<int> seq;
+    float cl = u2f(0x7f800000u);
+    uint32_t wn = G::NONE;
+    bin_walk_nodes(P, src, r, W.root, cl, wn, seq);
+    if (f2u(cl) != f2u(bin_closest) || wn != bin_winner) g_ws.mismatch++;
+    if (v.global.size() < seq.size()) v.global.resize(seq.size(), 0);
+    for (size_t k = 0; k < seq.size(); k++)
+      for (int b = 0; b < 3; b++)
+        if (!W.hot[b][seq[k]]) v.global[k] |= (uint8_t)(1u << b);
+  }
   v.bin_max = std::max(v.bin_max, bin_steps);
   v.wide_max = std::max(v.wide_max, wide_dep);
   v.bin_sum += bin_steps;
@@ -226,7 +263,10 @@ void render_pixel(const KParams& P, uint32_t px, uint32_t py, float* rgba, uint6
             src.base = P.walk;
           src.half = P.walk_half;
             const uint32_t nodes0 = cn.nodes, prims0 = cn.prims;
-            while (node < P.walk_end) walk_step_host<true>(P, src, node, r, closest, winner, cn);
+            if (P.walk_c16)
+              while (node < P.walk_end) walk_step_host<true, true>(P, src, node, r, closest, winner, cn);
+            else
+              while (node < P.walk_end) walk_step_host<true>(P, src, node, r, closest, winner, cn);
             if (g_wide && node != G::NONE) wide_price_segment(P, src, r, closest, winner, cn.nodes - nodes0, cn.prims - prims0, px, py, sample);
           } else {
             while (node < P.main_end) basic_step<CULL, true>(P, P.nodes, P.prims, node, r, closest, winner, cn);
@@ -309,9 +349,11 @@ int lane_sim_render(const void* blob, const hrt_blob_info* bi, const hrt_camera*
   P.motion_span = bi->motion_span;
   P.walk = base + bi->off_walk;
   P.walk_bytes = bi->walk_bytes;
-  P.walk_end = bi->walk_bytes;
+  P.walk_end = bi->walk_c16 ? bi->walk_nodes : bi->walk_bytes; /* layout.h WALK_C16: node indices */
   P.walk_hot = bi->walk_hot;
   P.walk_half = bi->walk_half ? bi->walk_half : 16u;
+  P.walk_c16 = bi->walk_c16;
+  P.walk_pbase = bi->walk_pbase;
   P.cam_origin = v3(cam->origin[0], cam->origin[1], cam->origin[2]);
   P.cam_llc = v3(cam->lower_left_corner[0], cam->lower_left_corner[1], cam->lower_left_corner[2]);
   P.cam_h = v3(cam->horizontal[0], cam->horizontal[1], cam->horizontal[2]);
@@ -365,20 +407,31 @@ int lane_sim_render(const void* blob, const hrt_blob_info* bi, const hrt_camera*
 
 /* Price the 4-wide walk over the sphere scene's walk stream on a region (render_basic_kernel's lane, EXACT):
  * renders the region as lane_sim_render (rgba, cnt), and for every segment walks the wide hierarchy too.
- * out[0..11]: segments, binary node steps, binary leaf tests, wide records, wide climbs, wide box tests, wide
+ * out[0..15]: segments, binary node steps, binary leaf tests, wide records, wide climbs, wide box tests, wide
  * leaf tests, segments whose wide result differs (must be 0), deepest trail, lockstep groups, sum over groups
- * of 64 x the binary max steps, of 64 x the wide max dependent loads (records + climbs).  arity 2: records of
+ * of 64 x the binary max steps, of 64 x the wide max dependent loads (records + climbs), lockstep binary steps,
+ * and those of them where some lane reads a node part not staged in LDS under each of HOT_BUDGETS.  arity 2: records of
  * the two child boxes of a node (no collapse), 4: of its grandchildren. */
 int lane_sim_wide_price(const void* blob, const hrt_blob_info* bi, const hrt_camera* cam, const hrt_render_params* p,
                         uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, float* rgba, uint64_t* cnt, uint64_t* out,
                         int arity) {
-  if (bi->walk_bytes == 0 || bi->walk_general || (arity != 2 && arity != 4)) return 1;
+  if (bi->walk_bytes == 0 || bi->walk_general || bi->walk_c16 || (arity != 2 && arity != 4)) return 1;
   g_wide_arity = arity;
   WideTree W;
   WalkSrc src;
   src.base = (const uint8_t*)blob + bi->off_walk;
   src.half = bi->walk_half ? bi->walk_half : 16u;
   W.root = wide_parse(src, 0u, W);
+  { /* the staged sets under each budget, by the builder's rule (largest parent box first, then depth) */
+    std::vector<int> order(W.T.size());
+    for (size_t i = 0; i < order.size(); i++) order[i] = (int)i;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+      return W.T[x].key != W.T[y].key ? W.T[x].key > W.T[y].key : W.T[x].depth < W.T[y].depth;
+    });
+    W.hot.assign(3, std::vector<char>(W.T.size(), 0));
+    for (int b = 0; b < 3; b++)
+      for (size_t k = 0; k < order.size() && k < HOT_BUDGETS[b]; k++) W.hot[b][order[k]] = 1;
+  }
   std::map<LockKey, LockVal> lock;
   std::map<uint64_t, uint32_t> segidx;
   g_wide = &W;
@@ -389,14 +442,17 @@ int lane_sim_wide_price(const void* blob, const hrt_blob_info* bi, const hrt_cam
   g_wide = nullptr;
   g_lock = nullptr;
   g_segidx = nullptr;
-  uint64_t groups = 0, bmax = 0, wmax = 0;
+  uint64_t groups = 0, bmax = 0, wmax = 0, lsteps = 0, lglob[3] = {0, 0, 0};
   for (const auto& kv : lock) {
     groups++;
     bmax += 64ull * kv.second.bin_max;
     wmax += 64ull * kv.second.wide_max;
+    lsteps += kv.second.global.size();
+    for (uint8_t g : kv.second.global)
+      for (int b = 0; b < 3; b++) lglob[b] += (g >> b) & 1u;
   }
-  const uint64_t v[12] = {g_ws.segs, g_ws.bin_steps, g_ws.bin_leaf, g_ws.wide_records, g_ws.wide_climbs, g_ws.wide_tests,
-                          g_ws.wide_leaf, g_ws.mismatch, g_ws.depth_max, groups, bmax, wmax};
+  const uint64_t v[16] = {g_ws.segs, g_ws.bin_steps, g_ws.bin_leaf, g_ws.wide_records, g_ws.wide_climbs, g_ws.wide_tests,
+                          g_ws.wide_leaf, g_ws.mismatch, g_ws.depth_max, groups, bmax, wmax, lsteps, lglob[0], lglob[1], lglob[2]};
   memcpy(out, v, sizeof(v));
   return rc;
 }

@@ -362,3 +362,32 @@ def test_c5_rank3_share_tile_vs_oracle(earth):
     """C5 (Cornell 2048^2, 10000 spp): a 256-px tile of rank 3's share (inside the room) against the oracle
     at full spp."""
     _share_tiles_vs_oracle("cornell", 2048, 2048, 10000, 3, [(1300, 700)], earth)
+
+
+@pytest.mark.gpu
+def test_c4_c16_stream_equals_32b_stream(earth, monkeypatch):
+    """C4's hybrid walk over 16-B node parts (layout.h WALK_C16, the default for random_10k: twice the node
+    parts staged in LDS) against the same walk over 32-B parts (HRT_WALK_C16=0 at commit): bit-identical pixels
+    and equal ray counts on every 16th tile of rank 2's 1/8 share at full spp."""
+    import torch
+
+    from hrt import tiling
+
+    W, H, spp = 3840, 2160, 2000
+    tiles = tiling.split_tiles(W, H, 8, 2)[5::16]
+    out = []
+    for c16 in ("1", "0"):
+        monkeypatch.setenv("HRT_WALK_C16", c16)
+        s = hrt.preset("random_10k", 1, earth)
+        s.commit()
+        monkeypatch.delenv("HRT_WALK_C16")
+        assert hrt.scene_blob(s)[1].walk_c16 == (1 if c16 == "1" else 0)
+        cam = hrt.preset_camera(s.info, W, H)
+        p = hrt.params(W, H, spp, 50, 1, tuple(s.info.background))
+        d = torch.empty(tiling.share_pixels(tiles) * 4, dtype=torch.float32, device="cuda")
+        st = hrt.render_tiles_device(s, cam, p, tiles, d.data_ptr(), 0, want_stats=True)
+        out.append((d.cpu().numpy(), int(st.segments), hrt.last_launch()["kernel"]))
+    (a, ra, ka), (b, rb, kb) = out
+    print(f"C16 {ka}: {ra} rays; 32-B {kb}: {rb} rays")
+    assert "C16 = true" in ka and "C16 = false" in kb
+    assert ra == rb and np.array_equal(a, b)

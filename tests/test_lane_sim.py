@@ -530,3 +530,90 @@ def test_foggy_scene_media_shapes(sim, monkeypatch):
     rc, c, sc = sim_render_scene(sim, s2, 40, 24, 6, 3, CULL_EXACT)
     assert rc == 0
     assert sa == sc and np.array_equal(a, c)
+
+
+def _c16_boxes(blob, info):
+    """The 16-B walk stream's node boxes as [lo, hi] in the tree's pre-order (layout.h WALK_C16)."""
+    words = np.frombuffer(bytes(blob), np.uint32)[info.off_walk // 4:(info.off_walk + info.walk_bytes) // 4]
+    parts = words[:info.walk_nodes * 4].reshape(-1, 4)
+    halves = parts[:, :3].copy().view(np.float16).astype(np.float64).reshape(-1, 6)  # Cx Cy Cz Ex Ey Ez
+    C, E = halves[:, :3], halves[:, 3:]
+    out = []
+
+    def walk(j):
+        out.append((C[j] - E[j], C[j] + E[j]))
+        p = int(parts[j, 3]) >> 16
+        if p & 0x8000:
+            return
+        walk(p)
+        walk(int(parts[p, 3]) & 0xFFFF)
+
+    walk(0)
+    return out
+
+
+def _b32_boxes(blob, info):
+    """The 32-B walk stream's node boxes [C - E, C + E] in the tree's pre-order (layout.h)."""
+    base = info.off_walk
+    raw = bytes(blob)[base:base + info.walk_bytes]
+    out = []
+
+    def part(off):
+        return np.frombuffer(raw[off:off + 32], np.float32), np.frombuffer(raw[off:off + 32], np.uint32)
+
+    def walk(off):
+        f, u = part(off)
+        C, E = f[:3].astype(np.float64), f[4:7].astype(np.float64)
+        out.append((C - E, C + E))
+        if u[7] & 0x80000000:
+            return
+        walk(int(u[7]))
+        walk(int(part(int(u[7]))[1][3]))
+
+    walk(0)
+    return out
+
+
+def test_c16_stream_boxes_hold_the_32b_boxes_and_nest(monkeypatch):
+    """layout.h WALK_C16 (the hybrid sphere stream of random_10k, BASELINE config 4): every 16-B node part's
+    binary16 box holds the 32-B part's box of the same node (so the node's geometry: all the inflated test
+    needs), and every inner node's encoded box holds its children's encoded boxes (monotone inclusion, as in the
+    32-B stream); the tree, the links and twice the staged node parts in the same LDS bytes."""
+    import sys
+
+    sys.setrecursionlimit(10000)
+    s16 = hrt.preset("random_10k", 1, None)
+    b16, i16 = hrt.scene_blob(s16)
+    monkeypatch.setenv("HRT_WALK_C16", "0")
+    b32, i32 = hrt.scene_blob(hrt.preset("random_10k", 1, None))
+    monkeypatch.delenv("HRT_WALK_C16")
+    assert i16.walk_c16 == 1 and i32.walk_c16 == 0 and i16.walk_nodes == i32.walk_nodes
+    assert i16.walk_hot == i32.walk_hot and i16.walk_hot // 16 == 2 * (i32.walk_hot // 32)
+    bx16, bx32 = _c16_boxes(b16, i16), _b32_boxes(b32, i32)
+    assert len(bx16) == len(bx32) == i16.walk_nodes
+    for (l16, h16), (l32, h32) in zip(bx16, bx32):
+        assert (l16 <= l32).all() and (h16 >= h32).all()
+    # nesting: parent boxes hold children's, checked along the pre-order with the parsed structure
+    words = np.frombuffer(bytes(b16), np.uint32)[i16.off_walk // 4:(i16.off_walk + i16.walk_bytes) // 4]
+    parts = words[:i16.walk_nodes * 4].reshape(-1, 4)
+    halves = parts[:, :3].copy().view(np.float16).astype(np.float64).reshape(-1, 6)
+    lo, hi = halves[:, :3] - halves[:, 3:], halves[:, :3] + halves[:, 3:]
+    inner = np.nonzero((parts[:, 3] >> 16) & 0x8000 == 0)[0]
+    c0 = parts[inner, 3] >> 16
+    c1 = parts[c0, 3] & 0xFFFF
+    for c in (c0, c1):
+        assert (lo[inner] <= lo[c]).all() and (hi[inner] >= hi[c]).all()
+
+
+def test_c16_stream_renders_like_the_32b_stream(sim, earth, monkeypatch):
+    """The sphere lane over the 16-B stream (random_10k) against the 32-B stream: the same closest hits and
+    winners, so bit-identical pixels and equal ray counts; and against the oracle at the parity bar."""
+    region = (1600, 900, 32, 8)
+    a, sa = sim_render(sim, "random_10k", 3840, 2160, 6, 50, 3, earth, kernel=0, cull=CULL_EXACT, region=region)
+    monkeypatch.setenv("HRT_WALK_C16", "0")
+    b, sb = sim_render(sim, "random_10k", 3840, 2160, 6, 50, 3, earth, kernel=0, cull=CULL_EXACT, region=region)
+    monkeypatch.delenv("HRT_WALK_C16")
+    assert sa["segments"] == sb["segments"] and np.array_equal(a, b)
+    ref, cnt = oracle_render("random_10k", 3840, 2160, 6, 50, 3, earth, region=region)
+    assert sa["segments"] == cnt["segments"] and np.abs(a - ref).max() <= TOL
+    print("node visits: 16-B parts", sa["nodes"], "32-B parts", sb["nodes"])
