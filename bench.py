@@ -339,7 +339,7 @@ def roofline_obj(args, scene, cam, bg, tiles, p, out_ptr, stream, launch_ms, seg
         "bound": "valu_issue",
         "achieved": None, "peak": round(SIMDS * MAX_CLOCK_HZ / VALU_CYC / 1e9, 1), "unit": "Gwave-inst/s",
         "frac": None, "traffic": None,
-        "walk_lane_util": round(int(sc.node_visits) / max(1, int(sc.walk_slots)), 4) if sc.walk_slots else None,
+        "walk_lane_util": round(int(sc.walk_steps or sc.node_visits) / max(1, int(sc.walk_slots)), 4) if sc.walk_slots else None,
         "alg_bytes_per_launch": alg_bytes,
         "alg_bytes_per_ray": round(alg_bytes / max(1, seg_step), 1),
         "lds_frac": round(alg_bytes / launch_s / 1e9 / PEAK_LDS_GBS, 4),

@@ -108,13 +108,25 @@ constexpr uint32_t CLAIM_BLOCK = 64; /* items per atomicAdd on the work counter 
  * chunk_plan) ordered [tile][8x8 block][chunk][64 pixels], then the short tail chunks' chunk-major, so
  * the launch ends on short items; a block is one chunk of 64 neighbouring pixels.  A wave hands out its whole block before it claims another,
  * and its lanes retire only on an item past the end, so no item is left behind. */
+/* RECOMPUTE (the general walk kernel): the work division's uniform divisors pass through an opaque copy at every
+ * claim, so their reciprocals are computed where a claim needs them instead of being kept in vector registers
+ * across the whole persistent loop (the general kernel at its 128-VGPR cap spilled them; claims are rare next to
+ * node steps).  The lane's rank among the claiming lanes comes from v_mbcnt (no per-lane mask kept live). */
+#ifndef HRT_CLAIM_MBCNT
+#define HRT_CLAIM_MBCNT 1
+#endif
+template <bool RECOMPUTE = false>
 __device__ __forceinline__ void claim_work(const KParams& P, uint32_t lane, bool& has_item, bool& exhausted,
                                            Item& it, WaveBlock& wb) {
   const bool want = !has_item && !exhausted;
   const unsigned long long want_mask = __ballot(want);
   if (!want_mask) return;
   const uint32_t cnt = (uint32_t)__popcll(want_mask);
+#if HRT_CLAIM_MBCNT
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(want_mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want_mask, 0u));
+#else
   const uint32_t rank = (uint32_t)__popcll(want_mask & ((1ull << lane) - 1ull));
+#endif
   const uint32_t avail = wb.end - wb.next;
   uint32_t w = wb.next + rank;
   if (cnt > avail) { /* the block's rest, then a new block (cnt <= 64 = CLAIM_BLOCK) */
@@ -140,19 +152,25 @@ __device__ __forceinline__ void claim_work(const KParams& P, uint32_t lane, bool
    * row: its pixels' texels and partial sums stay in cache), then the tail items chunk-major
    * [tail chunk][tile][8x8 block][64 pixels]; px = the padded pixel, then its tile (tiles padded to one
    * stride: a division; else a binary search on pad_start) */
+  uint32_t chunk_head = P.chunk_head, pad_px = P.pad_px, tile_stride = P.tile_stride;
+  if constexpr (RECOMPUTE) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+s"(chunk_head), "+s"(pad_px), "+s"(tile_stride));
+#endif
+  }
   uint32_t c, px;
   if (w < P.head_items) {
-    const uint32_t g = w / (64u * P.chunk_head), rem = w - g * 64u * P.chunk_head;
+    const uint32_t g = w / (64u * chunk_head), rem = w - g * 64u * chunk_head;
     c = rem >> 6;
     px = g * 64u + (rem & 63u);
   } else {
-    const uint32_t t = w - P.head_items, k = t / P.pad_px;
-    c = P.chunk_head + k;
-    px = t - k * P.pad_px;
+    const uint32_t t = w - P.head_items, k = t / pad_px;
+    c = chunk_head + k;
+    px = t - k * pad_px;
   }
   uint32_t lo = 0;
-  if (P.tile_stride) {
-    lo = px / P.tile_stride;
+  if (tile_stride) {
+    lo = px / tile_stride;
   } else {
     uint32_t hi = P.n_tiles - 1;
     while (lo < hi) {
@@ -201,6 +219,7 @@ __device__ __forceinline__ void flush_counts(const KParams& P, const Counts& cn)
   atomicAdd(&P.stats[8], (unsigned long long)cn.prim_slots);
   atomicAdd(&P.stats[13], (unsigned long long)cn.park_slots);
   atomicAdd(&P.stats[14], (unsigned long long)cn.wait_slots);
+  atomicAdd(&P.stats[16], (unsigned long long)cn.steps);
 }
 
 __device__ __forceinline__ void flush_stats(const KParams& P, uint32_t n_seg, uint32_t n_samples, uint32_t n_pixels,

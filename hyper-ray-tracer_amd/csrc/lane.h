@@ -174,6 +174,8 @@ struct Counts {
   uint32_t walk_slots, shade_slots; /* lane slots of wave iterations: walk (node) loop, shading passes */
   uint32_t prim_slots;              /* lane slots of wave executions of the primitive block */
   uint32_t park_slots, wait_slots;  /* sphere kernel walk steps: lanes parked on a leaf / done, waiting to shade */
+  uint32_t steps;                   /* walk kernels: lane slots of the walk loop that stepped a node (nodes also counts
+                                       the nodes leaf programs test) */
 };
 
 struct TRay {
@@ -960,9 +962,11 @@ HRT_LANE_FI float perlin_noise_t(PN pn, Vec3 point) {
 #pragma unroll
   for (int idx = 0; idx < 8; idx++) {
     const int x = idx / 4, y = (idx / 2) % 2, z = idx % 2;
-    uint32_t px = pn->perm[0][(uint32_t)((i + x) & 255)];
-    uint32_t py = pn->perm[1][(uint32_t)((j + y) & 255)];
-    uint32_t pz = pn->perm[2][(uint32_t)((k + z) & 255)];
+    /* perlin_noise.rs:92-94 `(i + i_x) & 255` in i32, which wraps in a release build at i = i32::MAX (a
+     * saturated huge coordinate): the same bits in u32, without C++'s signed-overflow UB (UBSan, r05) */
+    uint32_t px = pn->perm[0][((uint32_t)i + (uint32_t)x) & 255u];
+    uint32_t py = pn->perm[1][((uint32_t)j + (uint32_t)y) & 255u];
+    uint32_t pz = pn->perm[2][((uint32_t)k + (uint32_t)z) & 255u];
     const uint32_t g_i = px ^ py ^ pz;
     const Vec3 g = v3(pn->ranvec[g_i][0], pn->ranvec[g_i][1], pn->ranvec[g_i][2]);
     Vec3 weight = v3(u - (float)x, v - (float)y, w - (float)z);

@@ -217,8 +217,9 @@ constexpr uint32_t WALK_NODE_BYTES = 32, WALK_PAYLOAD_BYTES = 96;
  * no faster on C2 (14 024 vs 14 038 Mrays/s, profiles/r04g_ab.txt), so the conflicts are not what
  * bounds the step. */
 constexpr uint32_t WALK_SPLIT_HALF = 16384;
-/* 16-B node parts (r05, WALK_C16; hybrid sphere streams, the C4 class): the staged budget holds twice the node
- * parts.  A part is four u32: (C.x | C.y << 16), (C.z | E.x << 16), (E.y | E.z << 16), (skip | pass << 16), C and
+/* 16-B node parts (r05, WALK_C16; hybrid sphere streams, the C4 class; opt-in HRT_WALK_C16=1: measured 8% slower
+ * on C4's 1/8 share, the binary16 widening and link decode cost more than twice the staged node parts save):
+ * the staged budget holds twice the node parts.  A part is four u32: (C.x | C.y << 16), (C.z | E.x << 16), (E.y | E.z << 16), (skip | pass << 16), C and
  * E in IEEE binary16 (C rounded to nearest, E rounded up after adding C's rounding error, so the part's box
  * holds the 32-B part's box and with it the node's geometry: all the inflated test needs), the links 16-bit
  * node indices: node k's part at byte 16 k, the end = the node count N; pass of a leaf = WALK_C16_LEAF | j, its

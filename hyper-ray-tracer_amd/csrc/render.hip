@@ -315,7 +315,7 @@ hrt_status hguard(F&& f) {
   }
 }
 
-constexpr size_t SLOT_HDR = 256; /* work counter (8 B), stats words 0-11, error word 12, stats words 13-15 */
+constexpr size_t SLOT_HDR = 256; /* work counter (8 B), stats words 0-11, error word 12, stats words 13-16 */
 
 constexpr const char* SLOT_ERROR_MSG =
     "a render launch on this scene stopped walks that did not terminate (corrupt scene data); its frame is incomplete";
@@ -736,10 +736,10 @@ hrt_status device_upload(hrt_scene* s, int device) {
       const auto t0 = std::chrono::steady_clock::now();
       device_walk_regroup(leaves, T, device);
       s->w_build_us = (uint32_t)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+      s->w_regroup_pending = false; /* placed and written as the host build's hierarchy is (16-B parts included) */
       walk_place_and_write(s, T, leaves);
       s->w_device_built = true;
       s->w_regrouped = true;
-      s->w_regroup_pending = false;
     }
     std::vector<uint8_t> blob = build_blob(s);
     const size_t off = blob.size();
@@ -939,7 +939,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     /* the stats words and the watchdog's error word (h[12]) come back after EVERY launch, so a killed
      * frame is reported even when the caller asked for no stats (take_slot_error) */
     unsigned long long* h = (unsigned long long*)sl.h_tiles;
-    hip_check(hipMemcpyAsync(h, (uint8_t*)scratch + 8, 128, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(stats)");
+    hip_check(hipMemcpyAsync(h, (uint8_t*)scratch + 8, 136, hipMemcpyDeviceToHost, stream), "hipMemcpyAsync(stats)");
     hip_check(hipEventRecord((hipEvent_t)sl.event, stream), "hipEventRecord(slot)");
     sl.used = true;
     if (stats) {
@@ -958,6 +958,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
       stats->park_slots = h[13];
       stats->wait_slots = h[14];
       stats->leaf_cycles = h[15];
+      stats->walk_steps = h[16];
     }
   });
 }

@@ -29,6 +29,9 @@ using namespace hrt::kern;
 namespace {
 
 constexpr int GWALK_WAVES = HRT_GWALK_WAVES;
+#ifndef HRT_GWALK_RECOMPUTE
+#define HRT_GWALK_RECOMPUTE 1 /* kernel_common.h claim_work<RECOMPUTE> */
+#endif
 
 /* WMEM: where the walk stream is read (WM_LDS: staged whole; WM_HYB: its top levels staged, the rest
  * through the buffer descriptor; WM_BUF: global memory).  LREF: the reference node stream and the
@@ -123,7 +126,7 @@ void render_gwalk_kernel(KParams P) {
 
   for (;;) {
     const bool had_item = has_item;
-    claim_work(P, lane, has_item, exhausted, it, wb);
+    claim_work<HRT_GWALK_RECOMPUTE != 0>(P, lane, has_item, exhausted, it, wb);
     if (has_item && !had_item) *slot_lds = it.slot;
     if (!__any(has_item || !exhausted)) break;
     if (has_item && !walking) {
@@ -162,6 +165,7 @@ void render_gwalk_kernel(KParams P) {
           if constexpr (COUNT) cn.walk_slots++;
           if (node < end) {
             walk_box<COUNT, WMEM>(ws, node, r, tmin_c, closest, cn);
+            if constexpr (COUNT) cn.steps++;
           } else if constexpr (COUNT) {
             if (walk_pending(node)) cn.park_slots++;
             else if (walking) cn.wait_slots++;

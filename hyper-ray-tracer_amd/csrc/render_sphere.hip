@@ -156,6 +156,7 @@ void render_basic_kernel(KParams P) {
       for (int u = 0; u < WALK_UNROLL; u++) {
         if constexpr (COUNT) cn.walk_slots++;
         if (node < end) {
+          if constexpr (COUNT) cn.steps++;
           if constexpr (WS) walk_box<COUNT, WMEM, HRT_BOX_FMA && ((WMEM != WM_HYB && !HEAVY) || HRT_BOX_FMA_ALL), false,
                                     SPLIT ? G::WALK_SPLIT_HALF : 16u, C16>(ws, node, r, tmin_c, closest, cn); /* no rects: no NaN hits (lane.h set_noinv) */
           else basic_box<CULL, COUNT, STRIDE>(P, nodes, node, r, closest, cn);

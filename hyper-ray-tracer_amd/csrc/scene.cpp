@@ -1199,8 +1199,11 @@ static bool walk_place_and_write_impl(hrt_scene* s, const std::vector<WNode>& T,
 }
 
 void walk_place_and_write(hrt_scene* s, const std::vector<WNode>& T, const std::vector<WalkLeaf>& leaves) {
-  const char* c16_env = knob_env("HRT_WALK_C16"); /* "0": keep the 32-B node parts (A/B) */
-  const bool c16 = !(c16_env && strcmp(c16_env, "0") == 0);
+  /* "1": 16-B node parts for hybrid sphere streams (opt-in: r05 measured them 8% slower on C4's 1/8 share,
+   * 6 357 -> 5 833 Mrays/s: the binary16 widening and the link decode add ~8 VALU to a node step, more than the
+   * doubled staged set saves; profiles/r05_c16_ab.txt) */
+  const char* c16_env = knob_env("HRT_WALK_C16");
+  const bool c16 = c16_env && strcmp(c16_env, "1") == 0;
   if (!walk_place_and_write_impl(s, T, leaves, c16)) walk_place_and_write_impl(s, T, leaves, false);
 }
 

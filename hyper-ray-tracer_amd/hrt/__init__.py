@@ -87,7 +87,7 @@ class RenderStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in ("segments", "samples", "pixels", "node_visits", "prim_tests", "tex_evals",
                                                       "walk_slots", "shade_slots", "prim_slots")] + \
         [("phase_cycles", ctypes.c_uint64 * 3), ("park_slots", ctypes.c_uint64), ("wait_slots", ctypes.c_uint64),
-         ("leaf_cycles", ctypes.c_uint64)]
+         ("leaf_cycles", ctypes.c_uint64), ("walk_steps", ctypes.c_uint64)]
 
 
 class TilePixels(ctypes.Structure):

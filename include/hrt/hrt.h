@@ -121,6 +121,9 @@ typedef struct hrt_render_stats {
   uint64_t wait_slots;      /* ... spent with the walk done, waiting for the wave to leave the walk and shade */
   uint64_t leaf_cycles;     /* HRT_RENDER_COUNT_WORK, walk kernels: the part of phase_cycles[1] spent in the batched
                                leaf tests (sphere tests / leaf programs) */
+  uint64_t walk_steps;      /* HRT_RENDER_COUNT_WORK, walk kernels: lane slots of the walk loop that stepped a node
+                               (walk_steps / walk_slots = the walk's SIMD lane utilisation; node_visits also counts
+                               the nodes leaf programs test) */
 } hrt_render_stats;
 
 /* Scene description of one reference preset (application.rs:132-211). */

@@ -214,9 +214,11 @@ struct PerlinNoise {
     Vec3 c[2][2][2];
     for (int index = 0; index < 8; index++) {
       int i_x = index / 4, i_y = (index / 2) % 2, i_z = index % 2;
-      uint32_t x = permutation_x[(uint32_t)((i + i_x) & (POINT_COUNT - 1))];
-      uint32_t y = permutation_y[(uint32_t)((j + i_y) & (POINT_COUNT - 1))];
-      uint32_t z = permutation_z[(uint32_t)((k + i_z) & (POINT_COUNT - 1))];
+      /* i32 `i + i_x` wraps in a Rust release build (i = i32::MAX after the saturating cast of a huge
+       * coordinate): the same bits in u32, without C++'s signed-overflow UB */
+      uint32_t x = permutation_x[((uint32_t)i + (uint32_t)i_x) & (uint32_t)(POINT_COUNT - 1)];
+      uint32_t y = permutation_y[((uint32_t)j + (uint32_t)i_y) & (uint32_t)(POINT_COUNT - 1)];
+      uint32_t z = permutation_z[((uint32_t)k + (uint32_t)i_z) & (uint32_t)(POINT_COUNT - 1)];
       c[i_x][i_y][i_z] = random_vectors[x ^ y ^ z];
     }
     float u = point.x - floorf(point.x);

@@ -85,7 +85,7 @@ for key in flag_sets:
         st = hrt.render_tiles_device(scenes[ce], cam, p, tiles, out.data_ptr(), 0, want_stats=True)
         clear_env(env)
         print(f"   count: nodes/ray {st.node_visits/st.segments:.2f} prims/ray {st.prim_tests/st.segments:.3f} "
-              f"walk-lane-util {st.node_visits/max(1, st.walk_slots):.3f} walk-iters/ray {st.walk_slots/st.segments:.1f} "
+              f"walk-lane-util {(getattr(st, 'walk_steps', 0) or st.node_visits)/max(1, st.walk_slots):.3f} walk-iters/ray {st.walk_slots/st.segments:.1f} "
               f"shade-passes/ray {st.shade_slots/st.segments:.3f} prim-blocks/ray {st.prim_slots/st.segments:.2f} (x64 lanes)", flush=True)
         pcs = list(st.phase_cycles)
         if sum(pcs):
@@ -93,8 +93,9 @@ for key in flag_sets:
                   f" (leaf tests {st.leaf_cycles / sum(pcs):.1%} of all, inside walk)", flush=True)
         if st.walk_slots:
             ws = st.walk_slots
-            print(f"   walk slots: stepping {st.node_visits/ws:.1%}  parked on a leaf {st.park_slots/ws:.1%}  "
-                  f"done, waiting to shade {st.wait_slots/ws:.1%}  no walk {1 - (st.node_visits + st.park_slots + st.wait_slots)/ws:.1%}",
+            steps = getattr(st, "walk_steps", 0) or st.node_visits  # node_visits also counts leaf-program nodes
+            print(f"   walk slots: stepping {steps/ws:.1%}  parked on a leaf {st.park_slots/ws:.1%}  "
+                  f"done, waiting to shade {st.wait_slots/ws:.1%}  no walk {1 - (steps + st.park_slots + st.wait_slots)/ws:.1%}",
                   flush=True)
 img = out.cpu().numpy()
 print("mean rgb", img[..., :3].mean(axis=(0, 1)), "finite", bool(np.isfinite(img).all()))

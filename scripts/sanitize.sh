@@ -6,11 +6,11 @@
 #      walk-stream builders, presets, image writer, knobs), the oracle and the host lane simulator built under
 #      clang AddressSanitizer + UndefinedBehaviorSanitizer and loaded in place of the ordinary builds
 #      (HRT_LIB, ORACLE_LIB, LANE_SIM_CFLAGS), the clang ASan runtime preloaded into Python.
-# Output: gpurun_out/sanitize_*.log (scratch); the summary goes into DESIGN.md.
+# Output: $SAN_OUT (default /tmp/hrt_sanitize)/sanitize_*.log; the summary goes into DESIGN.md.
 set -u
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 cd "$ROOT"
-OUT=$ROOT/gpurun_out
+OUT=${SAN_OUT:-/tmp/hrt_sanitize}
 mkdir -p "$OUT"
 RT=/opt/rocm/lib/llvm/lib/clang/22/lib/linux/libclang_rt.asan-x86_64.so
 

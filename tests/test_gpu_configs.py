@@ -366,9 +366,9 @@ def test_c5_rank3_share_tile_vs_oracle(earth):
 
 @pytest.mark.gpu
 def test_c4_c16_stream_equals_32b_stream(earth, monkeypatch):
-    """C4's hybrid walk over 16-B node parts (layout.h WALK_C16, the default for random_10k: twice the node
-    parts staged in LDS) against the same walk over 32-B parts (HRT_WALK_C16=0 at commit): bit-identical pixels
-    and equal ray counts on every 16th tile of rank 2's 1/8 share at full spp."""
+    """C4's hybrid walk over 16-B node parts (layout.h WALK_C16, opt-in with HRT_WALK_C16=1 at commit: twice the
+    node parts staged in LDS) against the default walk over 32-B parts: bit-identical pixels and equal ray counts
+    on every 16th tile of rank 2's 1/8 share at full spp."""
     import torch
 
     from hrt import tiling

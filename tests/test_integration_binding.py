@@ -162,12 +162,13 @@ def test_struct_sizes_and_offsets_match_c(tmp_path):
         assert [f for f, *_ in py._fields_] == [f for f, _ in fields], ("python binding", name)
 
 
-def test_render_stats_is_120_bytes():
-    """The struct the round-2 binding had short by 16 bytes (park_slots / wait_slots); r04 added leaf_cycles."""
+def test_render_stats_is_128_bytes():
+    """The struct the round-2 binding had short by 16 bytes (park_slots / wait_slots); r04 added leaf_cycles, r05
+    walk_steps (the walk's own node steps: node_visits also counts the nodes leaf programs test)."""
     ds, _, _ = doc_api()
     names = [f for f, _ in ds["hrt_render_stats"]]
-    assert names[-3:] == ["park_slots", "wait_slots", "leaf_cycles"]
-    assert ctypes.sizeof(hrt.RenderStats) == 120
+    assert names[-4:] == ["park_slots", "wait_slots", "leaf_cycles", "walk_steps"]
+    assert ctypes.sizeof(hrt.RenderStats) == 128
 
 
 @pytest.mark.parametrize("name", ["hrt_scene_synchronize", "hrt_scene_get_info", "hrt_render_device", "hrt_preset_build"])

@@ -575,18 +575,18 @@ def _b32_boxes(blob, info):
 
 
 def test_c16_stream_boxes_hold_the_32b_boxes_and_nest(monkeypatch):
-    """layout.h WALK_C16 (the hybrid sphere stream of random_10k, BASELINE config 4): every 16-B node part's
+    """layout.h WALK_C16 (opt-in, HRT_WALK_C16=1; the hybrid sphere stream of random_10k, BASELINE config 4): every 16-B node part's
     binary16 box holds the 32-B part's box of the same node (so the node's geometry: all the inflated test
     needs), and every inner node's encoded box holds its children's encoded boxes (monotone inclusion, as in the
     32-B stream); the tree, the links and twice the staged node parts in the same LDS bytes."""
     import sys
 
     sys.setrecursionlimit(10000)
+    monkeypatch.setenv("HRT_WALK_C16", "1")  # opt-in (layout.h WALK_C16)
     s16 = hrt.preset("random_10k", 1, None)
     b16, i16 = hrt.scene_blob(s16)
-    monkeypatch.setenv("HRT_WALK_C16", "0")
-    b32, i32 = hrt.scene_blob(hrt.preset("random_10k", 1, None))
     monkeypatch.delenv("HRT_WALK_C16")
+    b32, i32 = hrt.scene_blob(hrt.preset("random_10k", 1, None))
     assert i16.walk_c16 == 1 and i32.walk_c16 == 0 and i16.walk_nodes == i32.walk_nodes
     assert i16.walk_hot == i32.walk_hot and i16.walk_hot // 16 == 2 * (i32.walk_hot // 32)
     bx16, bx32 = _c16_boxes(b16, i16), _b32_boxes(b32, i32)
@@ -609,10 +609,10 @@ def test_c16_stream_renders_like_the_32b_stream(sim, earth, monkeypatch):
     """The sphere lane over the 16-B stream (random_10k) against the 32-B stream: the same closest hits and
     winners, so bit-identical pixels and equal ray counts; and against the oracle at the parity bar."""
     region = (1600, 900, 32, 8)
+    monkeypatch.setenv("HRT_WALK_C16", "1")  # opt-in (layout.h WALK_C16)
     a, sa = sim_render(sim, "random_10k", 3840, 2160, 6, 50, 3, earth, kernel=0, cull=CULL_EXACT, region=region)
-    monkeypatch.setenv("HRT_WALK_C16", "0")
-    b, sb = sim_render(sim, "random_10k", 3840, 2160, 6, 50, 3, earth, kernel=0, cull=CULL_EXACT, region=region)
     monkeypatch.delenv("HRT_WALK_C16")
+    b, sb = sim_render(sim, "random_10k", 3840, 2160, 6, 50, 3, earth, kernel=0, cull=CULL_EXACT, region=region)
     assert sa["segments"] == sb["segments"] and np.array_equal(a, b)
     ref, cnt = oracle_render("random_10k", 3840, 2160, 6, 50, 3, earth, region=region)
     assert sa["segments"] == cnt["segments"] and np.abs(a - ref).max() <= TOL
