@@ -1,0 +1,140 @@
+"""Price a ray-distribution-aware hierarchy over the walk stream's fixed leaf order, before building it.
+
+The sphere kernel may walk ANY binary hierarchy over the reference's leaf sequence whose boxes hold their leaves
+(DESIGN.md section 4).  scene.cpp walk_regroup_dp picks the one minimising sum over inner nodes of 2 x half area
+(the surface-area stand-in for the probability that a ray reaches the node).  This script measures that
+probability directly on real segments instead: every segment of a few rows of a sphere-lane render (origin,
+direction, final closest; tests/native/lane_sim.hip lane_sim_segments) is tested against the inflated box of every
+leaf range (lane_sim_range_pass), and the same DP is run with cost 2 x P(range).  Both trees are then priced on
+held-out segments: expected node visits per segment = 1 + sum over inner nodes of 2 P(node) (with the final
+closest, so a lower bound of the walk's visits).
+
+  python scripts/price_hierarchy.py [--preset random] [--rays 20000]
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "hyper-ray-tracer_amd"), ROOT, os.path.join(ROOT, "scripts")]
+import hrt  # noqa: E402
+from price_wide import build  # noqa: E402
+
+
+def leaf_boxes(blob, info):
+    """The walk stream's leaves in pre-order: their node parts' boxes [C - E, C + E]."""
+    raw = bytes(blob)[info.off_walk:info.off_walk + info.walk_bytes]
+    out = []
+
+    def walk(off):
+        f = np.frombuffer(raw[off:off + 32], np.float32)
+        u = np.frombuffer(raw[off:off + 32], np.uint32)
+        if u[7] & 0x80000000:
+            out.append(np.r_[f[:3] - f[4:7], f[:3] + f[4:7]])
+            return
+        walk(int(u[7]))
+        walk(int(np.frombuffer(raw[int(u[7]):int(u[7]) + 16], np.uint32)[3]))
+
+    sys.setrecursionlimit(100000)
+    walk(0)
+    return np.asarray(out, np.float32)
+
+
+def segments(L, s, blob, info, W, H, spp, rows, seed=1):
+    cam = hrt.preset_camera(s.info, W, H)
+    p = hrt.params(W, H, spp, 50, seed, tuple(s.info.background))
+    out = []
+    for y in rows:
+        cap = W * spp * 60
+        buf = np.zeros(cap * 7, np.float32)
+        n = L.lane_sim_segments(blob, ctypes.byref(info), ctypes.byref(cam), ctypes.byref(p), 0, y, W, 1,
+                                buf.ctypes.data_as(ctypes.c_void_p), cap)
+        assert n >= 0
+        out.append(buf[:min(n, cap) * 7].reshape(-1, 7))
+    return np.concatenate(out)
+
+
+def range_prob(L, boxes, rays, tmin=0.001):
+    n = len(boxes)
+    cnt = np.zeros((n, n + 1), np.uint32)
+    L.lane_sim_range_pass(boxes.ctypes.data_as(ctypes.c_void_p), n, rays.ctypes.data_as(ctypes.c_void_p), len(rays),
+                          ctypes.c_float(tmin), cnt.ctypes.data_as(ctypes.c_void_p))
+    return cnt.astype(np.float64) / len(rays)
+
+
+def half_areas(boxes):
+    n = len(boxes)
+    A = np.zeros((n, n + 1))
+    for i in range(n):
+        mn, mx = boxes[i, :3].astype(np.float64), boxes[i, 3:].astype(np.float64)
+        for j in range(i + 1, n + 1):
+            mn = np.minimum(mn, boxes[j - 1, :3])
+            mx = np.maximum(mx, boxes[j - 1, 3:])
+            e = mx - mn
+            A[i, j] = e[0] * e[1] + e[1] * e[2] + e[2] * e[0]
+    return A
+
+
+def dp(W):
+    """C[i, j] = min_k C[i, k] + C[k, j] + 2 W[i, j]; returns the split table."""
+    n = W.shape[0]
+    C = np.zeros((n + 1, n + 1))
+    K = np.zeros((n + 1, n + 1), np.int64)
+    for ln in range(2, n + 1):
+        for i in range(0, n - ln + 1):
+            j = i + ln
+            ks = np.arange(i + 1, j)
+            c = C[i, ks] + C[ks, j]
+            b = int(np.argmin(c))
+            C[i, j] = c[b] + 2.0 * W[i, j]
+            K[i, j] = ks[b]
+    return K
+
+
+def inner_ranges(K, n):
+    out, todo = [], [(0, n)]
+    while todo:
+        i, j = todo.pop()
+        if j - i < 2:
+            continue
+        out.append((i, j))
+        k = K[i, j]
+        todo += [(i, k), (k, j)]
+    return out
+
+
+def visits(P, ranges):
+    return 1.0 + sum(2.0 * P[i, j] for i, j in ranges)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--preset", default="random")
+    ap.add_argument("--rays", type=int, default=20000)
+    a = ap.parse_args()
+    L = build()
+    L.lane_sim_segments.restype = ctypes.c_int
+    s = hrt.preset(a.preset, 1, None)
+    blob, info = hrt.scene_blob(s)
+    boxes = leaf_boxes(blob, info)
+    n = len(boxes)
+    rng = np.random.default_rng(3)
+    train = segments(L, s, blob, info, 1920, 1080, 2, [int(y) for y in rng.choice(1080, 8, replace=False)])
+    test = segments(L, s, blob, info, 1920, 1080, 2, [int(y) for y in rng.choice(1080, 8, replace=False)], seed=7)
+    train = train[rng.choice(len(train), min(a.rays, len(train)), replace=False)]
+    test = test[rng.choice(len(test), min(a.rays, len(test)), replace=False)]
+    print(f"{a.preset}: {n} leaves, {len(train)} training and {len(test)} test segments", flush=True)
+    Ptr = range_prob(L, boxes, train)
+    Pte = range_prob(L, boxes, test)
+    K_sa = dp(half_areas(boxes))
+    K_p = dp(Ptr)
+    r_sa, r_p = inner_ranges(K_sa, n), inner_ranges(K_p, n)
+    print(f"expected node visits per segment (final closest, test rays): surface-area DP {visits(Pte, r_sa):.2f}, "
+          f"ray-probability DP {visits(Pte, r_p):.2f} (in-sample {visits(Ptr, r_p):.2f})")
+
+
+if __name__ == "__main__":
+    main()

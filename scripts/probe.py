@@ -22,6 +22,8 @@ ap.add_argument("--env", default="", help="/-list of NAME=VALUE[,NAME=VALUE] env
 ap.add_argument("--commit-env", default="", help="/-list of NAME=VALUE[,...] env settings applied while the scene is "
                 "committed (walk-stream placement knobs): one scene per setting, alternated (A/B)")
 ap.add_argument("--count", action="store_true", help="also run one instrumented pass per variant")
+ap.add_argument("--options", default="", help="/-list of NAME=VALUE[,...] hrt_scene_options (chunk_min, chunk_max, "
+                "chunk_uniform, walk_tree, bvh_ties): one scene per setting, alternated (A/B)")
 ap.add_argument("--share", type=int, default=1, help="render rank 0's share of an N-way tile split (hrt/tiling.py)")
 a = ap.parse_args()
 
@@ -40,11 +42,17 @@ def clear_env(e):
 
 
 scenes = {}
-for ce in (a.commit_env.split("/") if a.commit_env else [""]):
-    set_env(ce)
-    sc = hrt.preset(a.preset, 1, hrt.load_image(_earth) if os.path.exists(_earth) else None)
+variants = [("env", ce) for ce in (a.commit_env.split("/") if a.commit_env else [""])]
+if a.options:
+    variants = [("opt", o) for o in a.options.split("/")]
+for kind, ce in variants:
+    opts = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in filter(None, ce.split(","))} if kind == "opt" else None
+    if kind == "env":
+        set_env(ce)
+    sc = hrt.preset(a.preset, 1, hrt.load_image(_earth) if os.path.exists(_earth) else None, options=opts)
     sc.commit(0)
-    clear_env(ce)
+    if kind == "env":
+        clear_env(ce)
     scenes[ce] = sc
     si = sc.scene_info()
     print(f"scene {a.preset} [{ce}]: nodes {si.nodes} prims {si.prims} features {si.feature_mask:#x} cull {si.cull_mode} blob {si.blob_bytes} B", flush=True)

@@ -5,11 +5,16 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# scripts/sanitize.sh preloads the clang ASan runtime into the test process itself; the compilers and helper
-# programs the tests start run without it (clang under a preloaded ASan runtime reports its own mmapped
-# sources as crashes)
-if "libclang_rt.asan" in os.environ.get("LD_PRELOAD", ""):
-    os.environ["HRT_SANITIZER_PRELOAD"] = os.environ.pop("LD_PRELOAD")
+
+
+def tool_env():
+    """The environment for the compilers the tests run: scripts/sanitize.sh preloads the clang ASan runtime into
+    the test processes (they load ASan-built libraries), and clang under a preloaded ASan runtime reports its own
+    mmapped sources as crashes, so compilers run without it."""
+    env = dict(os.environ)
+    if "libclang_rt.asan" in env.get("LD_PRELOAD", ""):
+        env.pop("LD_PRELOAD")
+    return env
 sys.path.insert(0, os.path.join(ROOT, "hyper-ray-tracer_amd"))
 sys.path.insert(0, ROOT)
 

@@ -61,6 +61,8 @@ struct WideStats {
   uint64_t lock_steps, lock_global[3]; /* lockstep binary steps; those where some lane reads a non-staged part */
 };
 WideTree* g_wide = nullptr;
+/* segment recorder (scripts/price_hierarchy.py): origin, direction, final closest of every sphere-lane segment */
+std::vector<float>* g_segs = nullptr;
 int g_wide_arity = 4; /* 2: a record holds its node's two child boxes (no collapse) */
 WideStats g_ws;
 struct LockKey {
@@ -268,6 +270,8 @@ void render_pixel(const KParams& P, uint32_t px, uint32_t py, float* rgba, uint6
             else
               while (node < P.walk_end) walk_step_host<true>(P, src, node, r, closest, winner, cn);
             if (g_wide && node != G::NONE) wide_price_segment(P, src, r, closest, winner, cn.nodes - nodes0, cn.prims - prims0, px, py, sample);
+            if (g_segs && node != G::NONE)
+              g_segs->insert(g_segs->end(), {r.o.x, r.o.y, r.o.z, r.d.x, r.d.y, r.d.z, closest});
           } else {
             while (node < P.main_end) basic_step<CULL, true>(P, P.nodes, P.prims, node, r, closest, winner, cn);
           }
@@ -455,6 +459,51 @@ int lane_sim_wide_price(const void* blob, const hrt_blob_info* bi, const hrt_cam
                           g_ws.wide_leaf, g_ws.mismatch, g_ws.depth_max, groups, bmax, wmax, lsteps, lglob[0], lglob[1], lglob[2]};
   memcpy(out, v, sizeof(v));
   return rc;
+}
+
+/* For every range [i, j) of a leaf sequence (boxes n x (mn, mx)), how many of the rays (m x (o, d, closest))
+ * pass the walk's inflated test (lane.h box_ce, fused form) of the range's union box on [tmin, closest]:
+ * out[i * (n + 1) + j].  Pricing hierarchies over a fixed leaf order (scripts/price_hierarchy.py). */
+int lane_sim_range_pass(const float* boxes, uint32_t n, const float* rays, uint32_t m, float tmin, uint32_t* out) {
+  std::vector<TRay> R(m);
+  std::vector<float> cl(m);
+  for (uint32_t q = 0; q < m; q++) {
+    set_dir(R[q], v3(rays[7 * q], rays[7 * q + 1], rays[7 * q + 2]), v3(rays[7 * q + 3], rays[7 * q + 4], rays[7 * q + 5]));
+    cl[q] = rays[7 * q + 6];
+  }
+  for (uint32_t i = 0; i < n; i++) {
+    float mn[3] = {boxes[6 * i], boxes[6 * i + 1], boxes[6 * i + 2]}, mx[3] = {boxes[6 * i + 3], boxes[6 * i + 4], boxes[6 * i + 5]};
+    for (uint32_t j = i + 1; j <= n; j++) {
+      if (j > i + 1)
+        for (int k = 0; k < 3; k++) {
+          mn[k] = std::min(mn[k], boxes[6 * (j - 1) + k]);
+          mx[k] = std::max(mx[k], boxes[6 * (j - 1) + 3 + k]);
+        }
+      float C[3], E[3], fmn[3], fmx[3];
+      walkbox::ce_floored(mn, mx, C, E, fmn, fmx);
+      const float4 a = make_float4(C[0], C[1], C[2], 0.0f), b = make_float4(E[0], E[1], E[2], 0.0f);
+      uint32_t c = 0;
+      for (uint32_t q = 0; q < m; q++) c += box_ce<true, false>(a, b, R[q], tmin, cl[q]) ? 1u : 0u;
+      out[(size_t)i * (n + 1) + j] = c;
+    }
+  }
+  return 0;
+}
+
+/* Every segment of a region's sphere-lane render (EXACT): out[7 k ..] = origin, direction, final closest (+inf on a
+ * miss); returns the number of segments (all of them are counted; at most cap are written). */
+int lane_sim_segments(const void* blob, const hrt_blob_info* bi, const hrt_camera* cam, const hrt_render_params* p,
+                      uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, float* out, uint32_t cap) {
+  std::vector<float> segs;
+  std::vector<float> rgba((size_t)w * h * 4);
+  uint64_t cnt[8] = {0};
+  g_segs = &segs;
+  const int rc = lane_sim_render(blob, bi, cam, p, 0, G::CULL_EXACT, x0, y0, w, h, rgba.data(), cnt);
+  g_segs = nullptr;
+  if (rc) return -1;
+  const size_t n = segs.size() / 7;
+  memcpy(out, segs.data(), std::min<size_t>(n, cap) * 7 * sizeof(float));
+  return (int)n;
 }
 
 /* The culling property behind CULL_EXACT on single spheres: whenever the reference's

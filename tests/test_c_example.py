@@ -3,6 +3,7 @@ import os
 import subprocess
 
 import pytest
+from conftest import tool_env
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -13,7 +14,7 @@ def exe(tmp_path_factory):
     subprocess.run(["gcc", "-O2", "-std=c11", "-Wall", "-Werror", "-I" + os.path.join(ROOT, "include"),
                     os.path.join(ROOT, "examples", "render_random.c"), "-o", out,
                     "-L" + os.path.join(ROOT, "hyper-ray-tracer_amd", "lib"), "-lhrt",
-                    "-Wl,-rpath," + os.path.join(ROOT, "hyper-ray-tracer_amd", "lib")], check=True)
+                    "-Wl,-rpath," + os.path.join(ROOT, "hyper-ray-tracer_amd", "lib")], check=True, env=tool_env())
     return out
 
 
@@ -47,7 +48,7 @@ def exe_progressive(tmp_path_factory):
     subprocess.run(["gcc", "-O2", "-std=c11", "-Wall", "-Werror", "-I" + os.path.join(ROOT, "include"),
                     os.path.join(ROOT, "examples", "render_progressive.c"), "-o", out,
                     "-L" + os.path.join(ROOT, "hyper-ray-tracer_amd", "lib"), "-lhrt",
-                    "-Wl,-rpath," + os.path.join(ROOT, "hyper-ray-tracer_amd", "lib")], check=True)
+                    "-Wl,-rpath," + os.path.join(ROOT, "hyper-ray-tracer_amd", "lib")], check=True, env=tool_env())
     return out
 
 

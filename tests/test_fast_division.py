@@ -6,6 +6,7 @@ import subprocess
 
 import numpy as np
 import pytest
+from conftest import tool_env
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -14,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 def checker(tmp_path_factory):
     exe = str(tmp_path_factory.mktemp("divrn") / "div_rn_check")
     subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", exe, os.path.join(HERE, "native", "div_rn_check.c"), "-lm"],
-                   check=True)
+                   check=True, env=tool_env())
     return exe
 
 

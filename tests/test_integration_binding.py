@@ -13,6 +13,7 @@ import re
 import subprocess
 
 import pytest
+from conftest import tool_env
 
 import hrt
 
@@ -134,7 +135,7 @@ def _c_layout(structs, tmp_path):
     lines.append("  return 0;\n}")
     src, exe = tmp_path / "layout.c", tmp_path / "layout"
     src.write_text("\n".join(lines))
-    subprocess.check_call(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    subprocess.check_call(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], env=tool_env())
     out = {}
     for line in subprocess.check_output([str(exe)], text=True).splitlines():
         s, f, v = line.split()

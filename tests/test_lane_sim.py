@@ -21,6 +21,7 @@ import numpy as np
 import pytest
 
 import hrt
+from conftest import tool_env
 from oracle import oracle as O
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -39,7 +40,7 @@ def _build_sim(tmp_path_factory, extra=()):
                     "--offload-host-only", *extra, *os.environ.get("LANE_SIM_CFLAGS", "").split(),  # scripts/sanitize.sh
                     "-I" + os.path.join(ROOT, "include"),
                     "-I" + os.path.join(ROOT, "hyper-ray-tracer_amd", "csrc"),
-                    os.path.join(HERE, "native", "lane_sim.hip"), "-o", so], check=True)
+                    os.path.join(HERE, "native", "lane_sim.hip"), "-o", so], check=True, env=tool_env())
     L = ctypes.CDLL(so)
     L.lane_sim_render.restype = ctypes.c_int
     L.lane_sim_chunks.restype = ctypes.c_int
