@@ -96,6 +96,11 @@ def parse():
                          "one GPU, DESIGN.md section 9)")
     ap.add_argument("--allow-knobs", action="store_true",
                     help="print the line even when A/B environment knobs of the library are set (never for a headline)")
+    ap.add_argument("--chunks", choices=["auto", "frame"], default="auto",
+                    help="sample-chunk schedule (hrt_scene_options): 'frame' = the library's default for the frame; "
+                         "'auto' = that, or 8-sample chunks when one GPU renders at most a quarter of the frame (its "
+                         "launch ends sooner: C2's 1/8 share +6%%).  Every rank and the 1-GPU check frame use the "
+                         "same schedule, so the delivered frame stays bit-identical")
     ap.add_argument("--share", type=int, default=1,
                     help="one process: render rank 0's share of an N-way tile split (one GPU's part of an N-GPU frame)")
     ap.add_argument("--launch-record", default="",
@@ -147,6 +152,16 @@ def rank_devices(dev, rank, local, world):
 
 def distinct_devices(devices):
     return len({(d["pci"], d["uuid"]) for d in devices})
+
+
+def chunk_options(args, share):
+    """hrt_scene_options for the run's sample chunks (--chunks): a GPU rendering at most a quarter of the frame
+    sums each pixel's samples in chunks of at least 8 (at most 64 of them) instead of the frame default's 16 / 32:
+    the launch's last items are shorter (profiles/r05_share_chunks_ab.txt: C2's 1/8 share 12 337 -> 13 104
+    Mrays/s; the whole frame 14 825 -> 14 647, so one GPU keeps the default)."""
+    if args.chunks == "auto" and share >= 4:
+        return {"chunk_min": 8, "chunk_max": 64}
+    return None
 
 
 def knob_report(launch):
@@ -444,7 +459,9 @@ def main():
                          "(--one-device rehearses N ranks on one GPU)")
     turns = args.one_device and world > 1 and args.rehearsal == "turns"
 
-    scene = hrt.preset(args.preset, 1, earth_image())
+    share_of = world if (world > 1 and args.scaling == "tiles") else max(1, args.share)
+    options = chunk_options(args, share_of)
+    scene = hrt.preset(args.preset, 1, earth_image(), options=options)
     scene.commit(local)
     si = scene.scene_info()
     W, H = args.width, args.height
@@ -637,6 +654,7 @@ def main():
                 **({"share": f"rank 0 of a {share}-way tile split ({args.tile}-px tiles): one GPU's part of a {share}-GPU frame",
                     "share_pixels": n_px} if world == 1 and share > 1 else {}),
                 "cull_mode": {0: "reference", 1: "slab (approximate)", 2: "exact (reference test + provably safe culling)"}[si.cull_mode],
+                "sample_chunks": {**hrt.sample_chunks(scene, p), "options": options or "frame default"},
             },
             "launch": launch,
             "ranks": world,

@@ -135,8 +135,14 @@ __device__ __forceinline__ void claim_work(const KParams& P, uint32_t lane, bool
     const uint32_t size = wb.end >= P.claim_fine ? cnt - avail : CLAIM_BLOCK;
     const int leader = __ffsll((long long)want_mask) - 1;
     uint32_t base = 0;
+#if HRT_CLAIM_MBCNT
+    /* the leader is the wanting lane of rank 0 (no lane index kept live); its result read back by a readlane */
+    if (want && rank == 0u) base = atomicAdd(P.counter, size);
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+#else
     if ((int)lane == leader) base = atomicAdd(P.counter, size);
     base = __builtin_amdgcn_readfirstlane(__shfl(base, leader));
+#endif
     if (rank >= avail) w = base + (rank - avail);
     wb.next = base + (cnt - avail);
     wb.end = base + size;
