@@ -98,9 +98,9 @@ def parse():
                     help="print the line even when A/B environment knobs of the library are set (never for a headline)")
     ap.add_argument("--chunks", choices=["auto", "frame"], default="auto",
                     help="sample-chunk schedule (hrt_scene_options): 'frame' = the library's default for the frame; "
-                         "'auto' = that, or 8-sample chunks when one GPU renders at most a quarter of the frame (its "
-                         "launch ends sooner: C2's 1/8 share +6%%).  Every rank and the 1-GPU check frame use the "
-                         "same schedule, so the delivered frame stays bit-identical")
+                         "'auto' = that, or 8-sample chunks when one GPU renders at most a quarter of the frame in a "
+                         "short launch (its end comes sooner: C2's 1/8 share +6%%).  Every rank and the 1-GPU check "
+                         "frame use the same schedule, so the delivered frame stays bit-identical")
     ap.add_argument("--share", type=int, default=1,
                     help="one process: render rank 0's share of an N-way tile split (one GPU's part of an N-GPU frame)")
     ap.add_argument("--launch-record", default="",
@@ -154,12 +154,16 @@ def distinct_devices(devices):
     return len({(d["pci"], d["uuid"]) for d in devices})
 
 
+SHORT_LAUNCH_SAMPLES = 500e6  # below this many samples per GPU a launch's end is a visible part of it
+
+
 def chunk_options(args, share):
     """hrt_scene_options for the run's sample chunks (--chunks): a GPU rendering at most a quarter of the frame
-    sums each pixel's samples in chunks of at least 8 (at most 64 of them) instead of the frame default's 16 / 32:
-    the launch's last items are shorter (profiles/r05_share_chunks_ab.txt: C2's 1/8 share 12 337 -> 13 104
-    Mrays/s; the whole frame 14 825 -> 14 647, so one GPU keeps the default)."""
-    if args.chunks == "auto" and share >= 4:
+    in a short launch (under SHORT_LAUNCH_SAMPLES primary samples: C2's shares; not C4's or C5's, whose 1/8 shares
+    run for a second or more) sums each pixel's samples in chunks of at least 8 (at most 64 of them) instead of
+    the frame default's 16 / 32: the launch's last items are shorter (profiles/r05_share_chunks_ab.txt: C2's 1/8
+    share 12 337 -> 13 104 Mrays/s; the whole frame 14 825 -> 14 647, so one GPU keeps the default)."""
+    if args.chunks == "auto" and share >= 4 and args.width * args.height * args.spp / share < SHORT_LAUNCH_SAMPLES:
         return {"chunk_min": 8, "chunk_max": 64}
     return None
 

@@ -42,3 +42,18 @@ def test_pmc_key_names_the_share_and_rejects_counters_above_peak():
     ro = {"peak": peak, "achieved": None, "frac": None}
     bench.apply_pmc(ro, "k", None, 0.2, 1e9)
     assert ro["frac"] is None and ro["pmc_key"] == "k"
+
+
+def test_chunk_schedule_per_run():
+    """--chunks auto: 8-sample chunks only for a GPU rendering at most a quarter of the frame in a short launch
+    (C2's shares at 4 and 8 GPUs); one GPU, C2's halves and C4's / C5's long share launches keep the frame's."""
+    def args(w, h, spp, chunks="auto"):
+        return argparse.Namespace(width=w, height=h, spp=spp, chunks=chunks)
+    short = {"chunk_min": 8, "chunk_max": 64}
+    assert bench.chunk_options(args(1920, 1080, 500), 1) is None
+    assert bench.chunk_options(args(1920, 1080, 500), 2) is None
+    assert bench.chunk_options(args(1920, 1080, 500), 4) == short
+    assert bench.chunk_options(args(1920, 1080, 500), 8) == short
+    assert bench.chunk_options(args(1920, 1080, 500, "frame"), 8) is None
+    assert bench.chunk_options(args(3840, 2160, 2000), 8) is None   # C4: 2.07 G samples per GPU
+    assert bench.chunk_options(args(2048, 2048, 10000), 8) is None  # C5
