@@ -252,9 +252,25 @@ def cpu_leg(args, frame_rays_per_sample):
     return cb, rows, img, c
 
 
+def spread_tiles(tiles, n, W, H):
+    """Indices of n of a share's tiles spread over the frame in two dimensions: for each point of a
+    Hammersley set (x = (k + 1/2) / n, y = the golden-ratio sequence) the share tile nearest to it, not yet
+    picked.  (Evenly spaced list indices land in one tile column under the diagonal deal: C5's 1/8 share
+    then sampled only the frame's left edge, where every camera ray misses the box.)"""
+    phi = (5 ** 0.5 - 1) / 2
+    centre = [(x + w / 2, y + h / 2) for x, y, w, h in tiles]
+    picked = set()
+    for k in range(min(n, len(tiles))):
+        px, py = (k + 0.5) / n * W, ((0.5 + k * phi) % 1.0) * H
+        best = min((i for i in range(len(tiles)) if i not in picked),
+                   key=lambda i: (centre[i][0] - px) ** 2 + (centre[i][1] - py) ** 2)
+        picked.add(best)
+    return sorted(picked)
+
+
 def cpu_leg_tiles(args, tiles, frame_rays_per_sample):
-    """cpu_leg for one GPU's share of a tile split (the C4 / C5 config lines): the oracle on 16-px tiles spread
-    evenly over the share at the frame's full spp (each tile's rows in 8-px tasks on the usable cores), as many
+    """cpu_leg for one GPU's share of a tile split (the C4 / C5 config lines): the oracle on 16-px tiles of the
+    share spread over the frame (spread_tiles) at the frame's full spp (each tile's rows in 8-px tasks on the usable cores), as many
     as the CPU budget allows (at least one).  Returns (cpu_baseline dict, picked tile indices, the oracle's
     pixels of those tiles packed as the share is, oracle counters)."""
     import numpy as np
@@ -272,13 +288,13 @@ def cpu_leg_tiles(args, tiles, frame_rays_per_sample):
                                task_w=8)
         return img, c
 
-    probe = tiles[len(tiles) // 2]
+    probes = spread_tiles(tiles, 4, W, H)  # the cost of a tile varies across the frame: price four
     t0 = time.perf_counter()
-    _, c = tile_render(probe, 4)
-    rate = c["segments"] / max(1e-6, time.perf_counter() - t0)
-    per_tile = c["segments"] / 4 * args.spp
+    seg = sum(tile_render(tiles[i], 4)[1]["segments"] for i in probes)
+    rate = seg / max(1e-6, time.perf_counter() - t0)
+    per_tile = seg / len(probes) / 4 * args.spp
     n = max(1, min(len(tiles), int(args.cpu_seconds * rate / max(1.0, per_tile))))
-    picks = sorted({min(len(tiles) - 1, int((k + 0.5) * len(tiles) / n)) for k in range(n)})
+    picks = spread_tiles(tiles, n, W, H)
     t0 = time.perf_counter()
     imgs, tot = [], {}
     for i in picks:
@@ -294,7 +310,7 @@ def cpu_leg_tiles(args, tiles, frame_rays_per_sample):
         "cores": threads,
         "kind": "port",
         "label": "CPU restatement of the reference path (oracle/, not the reference binary)",
-        "sample": f"{len(picks)} of the share's {len(tiles)} 16-px tiles, spread evenly, at {args.spp} spp "
+        "sample": f"{len(picks)} of the share's {len(tiles)} 16-px tiles, spread over the frame, at {args.spp} spp "
                   f"({tot['samples']} samples, {tot['segments']} rays, {dt:.1f} s); reference aabb.rs culling",
         "segments_per_sample": round(seg_per_sample, 4),
         "frame_segments_per_sample": round(frame_rays_per_sample, 4),

@@ -478,7 +478,10 @@ template <bool COUNT>
 void launch_any(const hrt_scene* s, const Plan& pl, const KParams& kp, hipStream_t stream) {
   const size_t smem = pl.lds ? pl.smem : 0;
   if (pl.gwalk) {
-    launch_gwalk(COUNT, pl.gwalk_mem, pl.gwalk_lref, pl.trim, kp, s->device, stream, smem);
+    /* every chunk one sample (head of 1-sample chunks, no tail): render_gwalk_kernel's ONE instantiation */
+    const char* o1 = knob_env("HRT_GWALK_ONE"); /* A/B knob: "0" keeps the general chunk loop */
+    const bool one = kp.chunk == 1u && kp.chunk_first == 1u && kp.n_chunks == kp.chunk_head && !(o1 && strcmp(o1, "0") == 0);
+    launch_gwalk(COUNT, pl.gwalk_mem, pl.gwalk_lref, pl.trim, one, kp, s->device, stream, smem);
     return;
   }
   if (pl.fast) {

@@ -36,8 +36,12 @@ constexpr int GWALK_WAVES = HRT_GWALK_WAVES;
 /* WMEM: where the walk stream is read (WM_LDS: staged whole; WM_HYB: its top levels staged, the rest
  * through the buffer descriptor; WM_BUF: global memory).  LREF: the reference node stream and the
  * primitives that leaf programs read are staged in LDS behind the walk stream. */
-/* BIG: one 1024-thread workgroup per CU (a hybrid stream's staged part beyond LDS_SCENE_MAX_BYTES) */
-template <bool COUNT, int WMEM, bool LREF, int TRIM, bool BIG>
+/* BIG: one 1024-thread workgroup per CU (a hybrid stream's staged part beyond LDS_SCENE_MAX_BYTES).
+ * ONE: every chunk of the schedule is one sample (deep general scenes up to 64 spp, lane.h sample_chunk):
+ * a lane's work item is dead once its sample has started and its partial sum is that sample's radiance, so
+ * neither the item nor the chunk's running sum lives across the walk and shading (Final: 48 -> 32 B of
+ * scratch per lane; the spills that were left were per-segment writes, 3.9 GB per launch). */
+template <bool COUNT, int WMEM, bool LREF, int TRIM, bool BIG, bool ONE>
 __global__ __launch_bounds__((BIG ? 256 : 128) * GWALK_WAVES, GWALK_WAVES)
 void render_gwalk_kernel(KParams P) {
   extern __shared__ float4 lds_scene[];
@@ -133,7 +137,9 @@ void render_gwalk_kernel(KParams P) {
       start_sample(P, ps, it.pxy & 0xFFFFu, it.pxy >> 16, it.sample);
       walking = true;
       setup = true;
+      if constexpr (ONE) n_pixels += it.sample == 0u ? 1u : 0u; /* lane-local: a pixel's first chunk */
     }
+    if constexpr (ONE) it = Item{0u, 0u, 0u, 0u}; /* every started item: nothing of it is read again */
     if (setup) {
 #if HRT_RAY_REDERIVE
       r.o = ps.ro;
@@ -228,7 +234,18 @@ void render_gwalk_kernel(KParams P) {
         done = shade<true, COUNT, TRIM>(Q, ps, winner, closest, r.o, r.d, MEDIA ? r.time : r.tau, r.tau, cn) ||
                ps.depth_left == 0;
       }
-      if (done) {
+      if (done && ONE) {
+        walking = false;
+        node = G::NONE;
+        sample_done = true;
+        const Vec3 c = v3(0.0f, 0.0f, 0.0f) + ps.rad; /* the chunk's sum, as the general case forms it */
+        if (P.n_chunks == 1)
+          P.out[*slot_lds] = make_float4(sqrtf(c.x * scale), sqrtf(c.y * scale), sqrtf(c.z * scale), 1.0f);
+        else
+          P.partial[*slot_lds] = make_float4(c.x, c.y, c.z, 0.0f);
+        chunk_done = true;
+        has_item = false;
+      } else if (done) {
         walking = false;
         node = G::NONE;
         sum = sum + ps.rad; /* application.rs:448: samples of a chunk summed in order */
@@ -249,8 +266,11 @@ void render_gwalk_kernel(KParams P) {
     }
     n_seg += (uint32_t)__popcll(__ballot(traced));
     n_samples += (uint32_t)__popcll(__ballot(sample_done));
-    n_pixels += (uint32_t)__popcll(__ballot(chunk_done && it.sample_end <= P.chunk));
+    if constexpr (!ONE) n_pixels += (uint32_t)__popcll(__ballot(chunk_done && it.sample_end <= P.chunk));
     stamp(2);
+  }
+  if constexpr (ONE) { /* n_pixels counted per lane: the wave's sum */
+    for (int o = 32; o >= 1; o >>= 1) n_pixels += (uint32_t)__shfl_xor((int)n_pixels, o);
   }
   if (lane == 0) {
     atomicAdd(&P.stats[0], (unsigned long long)n_seg);
@@ -265,23 +285,26 @@ void render_gwalk_kernel(KParams P) {
   }
 }
 
-template <bool COUNT, int WMEM, bool LREF, int TRIM, bool BIG = false>
+template <bool COUNT, int WMEM, bool LREF, int TRIM, bool BIG = false, bool ONE = false>
 void launch_g(const KParams& kp, int device, hipStream_t stream, size_t smem) {
-  const void* fn = (const void*)render_gwalk_kernel<COUNT, WMEM, LREF, TRIM, BIG>;
+  const void* fn = (const void*)render_gwalk_kernel<COUNT, WMEM, LREF, TRIM, BIG, ONE>;
   const int block = (BIG ? 256 : 128) * GWALK_WAVES;
   KParams p = kp;
   p.lane_lds = (uint32_t)((smem + 15) & ~(size_t)15);
   const size_t total = p.lane_lds + (size_t)block * sizeof(uint32_t);
   const int grid = resident_grid(fn, block, device, total, true, __PRETTY_FUNCTION__);
-  hipLaunchKernelGGL((render_gwalk_kernel<COUNT, WMEM, LREF, TRIM, BIG>), dim3(grid), dim3(block), total, stream, p);
+  hipLaunchKernelGGL((render_gwalk_kernel<COUNT, WMEM, LREF, TRIM, BIG, ONE>), dim3(grid), dim3(block), total, stream, p);
   hip_check(hipGetLastError(), "render_gwalk_kernel launch");
 }
 
 template <bool COUNT, int TRIM>
-void launch_g_mem(int wmem, bool lref, const KParams& kp, int device, hipStream_t stream, size_t smem) {
+void launch_g_mem(int wmem, bool lref, bool one, const KParams& kp, int device, hipStream_t stream, size_t smem) {
   if (wmem == WM_LDS) lref ? launch_g<COUNT, WM_LDS, true, TRIM>(kp, device, stream, smem)
                            : launch_g<COUNT, WM_LDS, false, TRIM>(kp, device, stream, smem);
-  else if (wmem == WM_HYB && smem > G::LDS_SCENE_MAX_BYTES) launch_g<COUNT, WM_HYB, false, TRIM, true>(kp, device, stream, smem);
+  else if (wmem == WM_HYB && smem > G::LDS_SCENE_MAX_BYTES) {
+    one ? launch_g<COUNT, WM_HYB, false, TRIM, true, true>(kp, device, stream, smem)
+        : launch_g<COUNT, WM_HYB, false, TRIM, true, false>(kp, device, stream, smem);
+  }
   else if (wmem == WM_HYB) launch_g<COUNT, WM_HYB, false, TRIM>(kp, device, stream, smem);
   else launch_g<COUNT, WM_BUF, false, TRIM>(kp, device, stream, smem);
 }
@@ -290,7 +313,7 @@ void launch_g_mem(int wmem, bool lref, const KParams& kp, int device, hipStream_
 
 namespace hrt {
 
-void launch_gwalk(bool count, int wmem, bool lref, int trim, const KParams& kp, int device, hipStream_t stream,
+void launch_gwalk(bool count, int wmem, bool lref, int trim, bool one, const KParams& kp, int device, hipStream_t stream,
                   size_t smem) {
   /* instantiated trims: none, media, heavy textures, both; TRIM_PROGRAMS with none (Final) or both (Cornell) */
   if (trim & TRIM_PROGRAMS) {
@@ -298,19 +321,19 @@ void launch_gwalk(bool count, int wmem, bool lref, int trim, const KParams& kp, 
     if (base != 0 && base != (TRIM_MEDIA | TRIM_HEAVY_TEX)) trim = base;
   }
   if (count) {
-    if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX | TRIM_PROGRAMS)) launch_g_mem<true, TRIM_MEDIA | TRIM_HEAVY_TEX | TRIM_PROGRAMS>(wmem, lref, kp, device, stream, smem);
-    else if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX)) launch_g_mem<true, TRIM_MEDIA | TRIM_HEAVY_TEX>(wmem, lref, kp, device, stream, smem);
-    else if (trim == TRIM_MEDIA) launch_g_mem<true, TRIM_MEDIA>(wmem, lref, kp, device, stream, smem);
-    else if (trim == TRIM_HEAVY_TEX) launch_g_mem<true, TRIM_HEAVY_TEX>(wmem, lref, kp, device, stream, smem);
-    else if (trim == TRIM_PROGRAMS) launch_g_mem<true, TRIM_PROGRAMS>(wmem, lref, kp, device, stream, smem);
-    else launch_g_mem<true, 0>(wmem, lref, kp, device, stream, smem);
+    if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX | TRIM_PROGRAMS)) launch_g_mem<true, TRIM_MEDIA | TRIM_HEAVY_TEX | TRIM_PROGRAMS>(wmem, lref, one, kp, device, stream, smem);
+    else if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX)) launch_g_mem<true, TRIM_MEDIA | TRIM_HEAVY_TEX>(wmem, lref, one, kp, device, stream, smem);
+    else if (trim == TRIM_MEDIA) launch_g_mem<true, TRIM_MEDIA>(wmem, lref, one, kp, device, stream, smem);
+    else if (trim == TRIM_HEAVY_TEX) launch_g_mem<true, TRIM_HEAVY_TEX>(wmem, lref, one, kp, device, stream, smem);
+    else if (trim == TRIM_PROGRAMS) launch_g_mem<true, TRIM_PROGRAMS>(wmem, lref, one, kp, device, stream, smem);
+    else launch_g_mem<true, 0>(wmem, lref, one, kp, device, stream, smem);
   } else {
-    if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX | TRIM_PROGRAMS)) launch_g_mem<false, TRIM_MEDIA | TRIM_HEAVY_TEX | TRIM_PROGRAMS>(wmem, lref, kp, device, stream, smem);
-    else if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX)) launch_g_mem<false, TRIM_MEDIA | TRIM_HEAVY_TEX>(wmem, lref, kp, device, stream, smem);
-    else if (trim == TRIM_MEDIA) launch_g_mem<false, TRIM_MEDIA>(wmem, lref, kp, device, stream, smem);
-    else if (trim == TRIM_HEAVY_TEX) launch_g_mem<false, TRIM_HEAVY_TEX>(wmem, lref, kp, device, stream, smem);
-    else if (trim == TRIM_PROGRAMS) launch_g_mem<false, TRIM_PROGRAMS>(wmem, lref, kp, device, stream, smem);
-    else launch_g_mem<false, 0>(wmem, lref, kp, device, stream, smem);
+    if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX | TRIM_PROGRAMS)) launch_g_mem<false, TRIM_MEDIA | TRIM_HEAVY_TEX | TRIM_PROGRAMS>(wmem, lref, one, kp, device, stream, smem);
+    else if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX)) launch_g_mem<false, TRIM_MEDIA | TRIM_HEAVY_TEX>(wmem, lref, one, kp, device, stream, smem);
+    else if (trim == TRIM_MEDIA) launch_g_mem<false, TRIM_MEDIA>(wmem, lref, one, kp, device, stream, smem);
+    else if (trim == TRIM_HEAVY_TEX) launch_g_mem<false, TRIM_HEAVY_TEX>(wmem, lref, one, kp, device, stream, smem);
+    else if (trim == TRIM_PROGRAMS) launch_g_mem<false, TRIM_PROGRAMS>(wmem, lref, one, kp, device, stream, smem);
+    else launch_g_mem<false, 0>(wmem, lref, one, kp, device, stream, smem);
   }
 }
 

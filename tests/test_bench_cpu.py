@@ -57,3 +57,22 @@ def test_chunk_schedule_per_run():
     assert bench.chunk_options(args(1920, 1080, 500, "frame"), 8) is None
     assert bench.chunk_options(args(3840, 2160, 2000), 8) is None   # C4: 2.07 G samples per GPU
     assert bench.chunk_options(args(2048, 2048, 10000), 8) is None  # C5
+
+
+def test_share_tiles_for_the_cpu_leg_spread_in_two_dimensions():
+    """The oracle tiles of a share's CPU leg and parity band cover the frame in x and y.  Evenly spaced list
+    indices of rank 0's 1/8 share of C5 (2048^2, diagonal deal) all fell in the leftmost tile column, where
+    every camera ray misses the Cornell box (r05c: 1.0 rays per sample)."""
+    from hrt import tiling
+    for W, H, world, rank, n in ((2048, 2048, 8, 0, 8), (3840, 2160, 8, 5, 5), (1920, 1080, 2, 1, 4), (64, 48, 2, 1, 40)):
+        tiles = tiling.split_tiles(W, H, world, rank)
+        picks = bench.spread_tiles(tiles, n, W, H)
+        assert picks == sorted(set(picks)) and len(picks) == min(n, len(tiles))
+        assert all(0 <= i < len(tiles) for i in picks)
+        xs = {tiles[i][0] for i in picks}
+        ys = {tiles[i][1] for i in picks}
+        want_x = min(len(picks), 4, len({t[0] for t in tiles}))
+        want_y = min(len(picks), 4, len({t[1] for t in tiles}))
+        assert len(xs) >= want_x and len(ys) >= want_y, (W, H, world, rank, sorted(xs), sorted(ys))
+        span_x = max(xs) - min(xs)
+        assert len(picks) < 4 or span_x >= W / 2, (W, span_x)

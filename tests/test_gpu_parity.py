@@ -446,6 +446,30 @@ def test_final_walk_variants_are_bit_identical(earth, monkeypatch, knob):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("spp", [24, 1, 65])
+def test_final_one_sample_chunks_equal_the_chunk_loop(earth, monkeypatch, spp):
+    """render_gwalk_kernel's ONE instantiation (every chunk one sample: Final up to 64 spp; no work item or
+    running sum kept across the walk and shading) against the general chunk loop on the same schedule
+    (HRT_GWALK_ONE=0): the same pixels bit for bit, the same ray, sample and pixel counts.  spp 1 writes the
+    frame directly (one chunk); at 65 spp the schedule has 2-sample chunks and ONE is not chosen."""
+    w, h = 80, 48
+    s = hrt.preset("final", 1, earth)
+    s.commit()
+    cam = hrt.preset_camera(s.info, w, h)
+    p = hrt.params(w, h, spp, 50, 3, tuple(s.info.background))
+    a, sa = hrt.render(s, cam, p, stats=True)
+    ka = hrt.last_launch()["kernel"]
+    assert ("ONE = true" in ka) == (spp <= 64), ka
+    monkeypatch.setenv("HRT_GWALK_ONE", "0")
+    b, sb = hrt.render(s, cam, p, stats=True)
+    kb = hrt.last_launch()["kernel"]
+    assert "ONE = false" in kb, kb
+    assert (sa.segments, sa.samples, sa.pixels) == (sb.segments, sb.samples, sb.pixels)
+    assert sa.pixels == w * h and sa.samples == w * h * spp
+    assert np.array_equal(a, b)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name,w,h,spp", [("random", 64, 36, 100), ("cornell", 48, 48, 150)])
 def test_env_chunk_knobs_do_not_change_frame(earth, monkeypatch, name, w, h, spp):
     """the r04 environment knobs that regrouped each pixel's sum (HRT_CHUNK_MIN / DIV /
