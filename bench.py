@@ -101,6 +101,10 @@ def parse():
                          "'auto' = that, or 8-sample chunks when one GPU renders at most a quarter of the frame in a "
                          "short launch (its end comes sooner: C2's 1/8 share +6%%).  Every rank and the 1-GPU check "
                          "frame use the same schedule, so the delivered frame stays bit-identical")
+    ap.add_argument("--view", choices=["camera", "none"], default="camera",
+                    help="hrt_scene_set_view before commit: 'camera' = the rendered camera (a walk stream beyond LDS "
+                         "stages the node parts its rays visit most: C4, Final), 'none' = the largest-box ranking.  "
+                         "Same image bit for bit either way")
     ap.add_argument("--share", type=int, default=1,
                     help="one process: render rank 0's share of an N-way tile split (one GPU's part of an N-GPU frame)")
     ap.add_argument("--launch-record", default="",
@@ -482,10 +486,13 @@ def main():
     share_of = world if (world > 1 and args.scaling == "tiles") else max(1, args.share)
     options = chunk_options(args, share_of)
     scene = hrt.preset(args.preset, 1, earth_image(), options=options)
-    scene.commit(local)
-    si = scene.scene_info()
     W, H = args.width, args.height
     cam = hrt.preset_camera(scene.info, W, H)
+    if args.view == "camera":  # placement hint: the staged part of a stream beyond LDS (never the image)
+        scene.set_view(cam)
+    scene.commit(local)
+    si = scene.scene_info()
+    blob_info = hrt.scene_blob(scene)[1]
     bg = tuple(scene.info.background)
     tiled = args.scaling == "tiles"
     share = world if (world > 1 and tiled) else max(1, args.share)
@@ -675,6 +682,10 @@ def main():
                     "share_pixels": n_px} if world == 1 and share > 1 else {}),
                 "cull_mode": {0: "reference", 1: "slab (approximate)", 2: "exact (reference test + provably safe culling)"}[si.cull_mode],
                 "sample_chunks": {**hrt.sample_chunks(scene, p), "options": options or "frame default"},
+                "placement": ({"staged": ("node parts the rendered camera's rays visit most (hrt_scene_set_view)"
+                                          if args.view == "camera" else "node parts under the largest boxes"),
+                               "staged_bytes": int(blob_info.walk_hot), "stream_bytes": int(blob_info.walk_bytes)}
+                              if blob_info.walk_hot else "the whole walk stream in LDS"),
             },
             "launch": launch,
             "ranks": world,

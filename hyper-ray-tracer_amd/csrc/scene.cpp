@@ -972,6 +972,45 @@ void walk_transcode_c16(hrt_scene* s, uint32_t N) {
   s->w_pbase = pbase;
 }
 
+/* How often camera rays through a VIEW_GRID x VIEW_GRID grid of the view's image plane (pinhole: lens and
+ * shutter ignored) visit each node of the walk hierarchy T (pre-order, T[i].end one past i's subtree), walked
+ * with T's boxes in f64 and stopped at the nearest LEAF BOX entered so far (a stand-in for the closest hit
+ * that needs no primitive code).  The placement's ranking only: any ranking gives the same image. */
+constexpr uint32_t VIEW_GRID = 128;
+static std::vector<uint32_t> view_heat(const hrt_camera& c, const std::vector<WNode>& T) {
+  const uint32_t N = (uint32_t)T.size();
+  std::vector<uint32_t> heat(N, 0);
+  const double tmin = 0.001;
+  for (uint32_t gy = 0; gy < VIEW_GRID; gy++)
+    for (uint32_t gx = 0; gx < VIEW_GRID; gx++) {
+      const double u = (gx + 0.5) / VIEW_GRID, v = (gy + 0.5) / VIEW_GRID;
+      double o[3], inv[3];
+      for (int k = 0; k < 3; k++) {
+        o[k] = c.origin[k];
+        const double d = (double)c.lower_left_corner[k] + u * c.horizontal[k] + v * c.vertical[k] - o[k];
+        inv[k] = 1.0 / d;
+      }
+      double closest = HUGE_VAL;
+      for (uint32_t i = 0; i < N;) {
+        heat[i]++;
+        double lo = tmin, hi = closest;
+        for (int k = 0; k < 3; k++) {
+          const double t0 = (T[i].box.mn[k] - o[k]) * inv[k], t1 = (T[i].box.mx[k] - o[k]) * inv[k];
+          const double a = std::min(t0, t1), b = std::max(t0, t1);
+          if (a == a) lo = std::max(lo, a); /* NaN (0 x inf: the origin on a slab plane) leaves the bound */
+          if (b == b) hi = std::min(hi, b);
+        }
+        if (lo <= hi) {
+          if (T[i].leaf >= 0) closest = std::min(closest, lo);
+          i++;
+        } else {
+          i = T[i].end;
+        }
+      }
+    }
+  return heat;
+}
+
 /* c16: a hybrid sphere stream is laid out for 16-B node parts: twice the node parts selected for the staged
  * set, then transcoded (walk_transcode_c16).  Returns false when that was asked for and could not be done
  * (the caller lays the stream out again without it). */
@@ -1007,7 +1046,24 @@ static bool walk_place_and_write_impl(hrt_scene* s, const std::vector<WNode>& T,
   if (hybrid) {
     std::vector<uint32_t> order(N);
     for (uint32_t i = 0; i < N; i++) order[i] = i;
-    if (by_area) {
+    if (s->has_view && by_area) {
+      /* hrt_scene_set_view: the node parts the view's camera rays visit most (lane-simulated C4 segments, held-out
+       * rows: 14.2 -> 1.6 of 73.7 node visits per segment outside LDS, scripts/price_hotset.py), then the
+       * largest parent box first among the rest */
+      const std::vector<uint32_t> heat = view_heat(s->view, T);
+      std::vector<double> key(N, 0.0);
+      key[0] = HUGE_VAL;
+      for (uint32_t i = 0; i < N; i++)
+        if (T[i].leaf < 0 && i + 1 < N) {
+          const double a = half_area(T[i].box);
+          key[i + 1] = a;
+          if (T[i + 1].end < N) key[T[i + 1].end] = a;
+        }
+      std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+        if (heat[a] != heat[b]) return heat[a] > heat[b];
+        return key[a] != key[b] ? key[a] > key[b] : T[a].depth < T[b].depth;
+      });
+    } else if (by_area) {
       std::vector<double> key(N, 0.0);
       key[0] = HUGE_VAL;
       for (uint32_t i = 0; i < N; i++)
@@ -2040,6 +2096,14 @@ hrt_status hrt_scene_set_options(hrt_scene* s, const hrt_scene_options* o) {
     need(o->bvh_ties <= 1 && o->walk_tree <= 1 && o->chunk_uniform <= 1, HRT_ERR_INVALID_ARG,
          "hrt_scene_set_options: bvh_ties, walk_tree and chunk_uniform are 0 or 1");
     s->opts = *o;
+  });
+}
+
+hrt_status hrt_scene_set_view(hrt_scene* s, const hrt_camera* view) {
+  return guard([&] {
+    mutable_scene(s);
+    s->has_view = view != nullptr;
+    s->view = view ? *view : hrt_camera{};
   });
 }
 

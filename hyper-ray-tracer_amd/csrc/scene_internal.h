@@ -105,6 +105,8 @@ struct hrt_scene {
   uint32_t n_media = 0;
   bool committed = false;
   hrt_scene_options opts{}; /* explicit configuration (hrt_scene_set_options); all-zero = default */
+  bool has_view = false;    /* placement hint (hrt_scene_set_view): the camera most renders will use */
+  hrt_camera view{};
 
   /* ---- flattened (valid after commit) ---- */
   std::vector<hrt::gpu::Node> g_nodes;

@@ -150,7 +150,7 @@ class SceneOptions(ctypes.Structure):
 
 # Diagnostics an older build may lack; only tolerated when HRT_LIB points at another build (A/B runs)
 OPTIONAL = {"hrt_last_launch", "hrt_debug_box_test", "hrt_scene_set_options", "hrt_scene_get_options",
-            "hrt_debug_sample_chunks"}
+            "hrt_debug_sample_chunks", "hrt_scene_set_view"}
 HRT_LIB_OVERRIDE = bool(os.environ.get("HRT_LIB"))
 
 # Every entry point of include/hrt/hrt.h (tests/test_abi.py checks the header against this list).
@@ -164,7 +164,7 @@ EXPORTS = [
     "hrt_render_tiles_device", "hrt_render_device", "hrt_render", "hrt_tile_grid", "hrt_scene_get_info", "hrt_last_launch", "hrt_debug_box_test",
     "hrt_debug_device_math", "hrt_debug_trace_path", "hrt_debug_scene_blob", "hrt_image_write", "hrt_render_progressive", "hrt_debug_prim_record",
     "hrt_scene_synchronize", "hrt_debug_poke_blob", "hrt_scene_set_options", "hrt_scene_get_options",
-    "hrt_debug_sample_chunks",
+    "hrt_debug_sample_chunks", "hrt_scene_set_view",
 ]
 
 _lib = None
@@ -239,6 +239,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "hrt_debug_poke_blob": (S, [vp, u64, vp, u64]),
         "hrt_scene_set_options": (S, [vp, ctypes.POINTER(SceneOptions)]),
         "hrt_scene_get_options": (S, [vp, ctypes.POINTER(SceneOptions)]),
+        "hrt_scene_set_view": (S, [vp, ctypes.POINTER(Camera)]),
         "hrt_debug_sample_chunks": (S, [vp, ctypes.POINTER(RenderParams), _U32P]),
     }
     for name, (res, args) in sig.items():
@@ -374,6 +375,13 @@ class Scene:
                 raise TypeError(f"unknown scene option {k!r}")
             setattr(o, k, int(v))
         _check(load().hrt_scene_set_options(self.h, ctypes.byref(o)))
+
+    def set_view(self, cam: Optional["Camera"]):
+        """hrt_scene_set_view: the camera most renders will use (None: no hint).  Placement only: which node parts
+        of a walk stream too large for LDS are staged there; the image is the same bit for bit."""
+        if cam is not None:
+            self._keep.append(cam)
+        _check(load().hrt_scene_set_view(self.h, ctypes.byref(cam) if cam is not None else None))
 
     def options(self) -> SceneOptions:
         o = SceneOptions()

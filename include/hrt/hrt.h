@@ -224,6 +224,13 @@ typedef struct hrt_scene_options {
 } hrt_scene_options;
 hrt_status hrt_scene_set_options(hrt_scene* s, const hrt_scene_options* options);
 hrt_status hrt_scene_get_options(const hrt_scene* s, hrt_scene_options* options);
+/* Placement hint (no reference counterpart; never changes an image's bits): the camera most renders of this
+ * scene will use (NULL: none, the default).  A walk stream too large for LDS keeps part of its node parts in
+ * LDS and reads the rest from global memory; with a view, hrt_scene_commit stages the node parts that camera
+ * rays through a 128 x 128 grid of the view's image plane visit most instead of those
+ * under the largest boxes.  Any placement renders the same image bit for bit.  Before commit (HRT_ERR_STATE
+ * after). */
+hrt_status hrt_scene_set_view(hrt_scene* s, const hrt_camera* view);
 
 hrt_status hrt_scene_set_root(hrt_scene* s, uint32_t node);
 /* Flatten + upload to HIP device `device` (-1: the calling thread's current device). */

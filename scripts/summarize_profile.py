@@ -10,8 +10,10 @@ bench.py reads for its `roofline` object:
   - lds_*       : SQ_INSTS_LDS, SQ_LDS_BANK_CONFLICT, SQ_LDS_IDX_ACTIVE;
   - lib_sha16   : which libhrt.so build the counters belong to (bench reports whether it matches);
   - launch      : bench.py's record of the launch (hrt_last_launch: kernel, grid, occupancy, VGPRs, scratch).
-The launch profiled is the first timed-kernel dispatch of the run (the warm-up frame with stats).
-A record whose SQ_WAVES differs from the waves the launch record says were launched (grid x block / 64) is
+The launch profiled is the first timed-kernel dispatch of the run (the warm-up frame with stats) whose SQ_WAVES
+equal the launch record's waves; the same dispatch (by its order among the timed kernel's dispatches) is read in
+every pass.  (r05c, C4's 8-s whole frame: the first dispatch reported SQ_WAVES 12288 against 6144 launched, with
+every other counter of every pass equal to the next two dispatches'.)  A record whose SQ_WAVES differs from the waves the launch record says were launched (grid x block / 64) is
 REJECTED: its counters describe another launch shape (a box whose occupancy answer differed, another
 build), so bench.py does not price a launch with them.
 """
@@ -75,14 +77,31 @@ def main():
     sq, sq2 = per_dispatch("sq"), per_dispatch("sq2")
     fetch, write = per_dispatch("fetch"), per_dispatch("write")
 
-    def timed(d):
+    launch = None
+    for name in ("sq2", "sq", "kt"):
+        lp = os.path.join(src, f"prof_{tag}_{name}", "launch.json")
+        if os.path.exists(lp):
+            launch = json.load(open(lp))
+            break
+    want = launch["grid"] * launch["block"] // 64 if launch else None
+
+    def dispatches(d):
+        """the timed kernel's dispatches of one pass, in order"""
         if kname is None:
-            return first_render(d)[1]
+            name, v = first_render(d)
+            return [v] if name else []
         short = kname.split("(")[0]
-        for (disp, name), v in sorted(d.items()):
-            if name.split("(")[0] == short:
-                return v
-        return {}
+        return [v for (disp, name), v in sorted(d.items()) if name.split("(")[0] == short]
+
+    ordinal = 0
+    for i, v in enumerate(dispatches(sq2)):
+        if want is not None and int(round(v.get("SQ_WAVES", -1))) == want:
+            ordinal = i
+            break
+
+    def timed(d):
+        ds = dispatches(d)
+        return ds[ordinal] if ordinal < len(ds) else (ds[0] if ds else {})
 
     s1, s2, f, w = timed(sq), timed(sq2), timed(fetch), timed(write)
     c = {**s1, **s2}
@@ -125,18 +144,12 @@ def main():
                 wc = c["SQ_WAVE_CYCLES"]
                 lines.append(f"\n**Wave time**: issuing {c['SQ_ACTIVE_INST_ANY']/wc*100:.1f}%, waiting to issue (pipe busy / "
                              f"dependency) {c['SQ_WAIT_INST_ANY']/wc*100:.1f}%, waiting on s_waitcnt {c['SQ_WAIT_ANY']/wc*100:.1f}%")
-    launch = None
-    for name in ("sq2", "sq", "kt"):
-        lp = os.path.join(src, f"prof_{tag}_{name}", "launch.json")
-        if os.path.exists(lp):
-            launch = json.load(open(lp))
-            break
     if launch:
         res["launch"] = launch
+        res["dispatch_ordinal"] = ordinal
         lines.append(f"\n**Launch** (hrt_last_launch): `{launch['kernel'][:120]}`, grid {launch['grid']} x {launch['block']} "
                      f"({launch['blocks_per_cu']} workgroups per CU x {launch['cus']} CUs, {launch['waves_per_simd']} waves/SIMD), "
                      f"{launch['vgprs']} VGPRs, {launch['scratch_bytes']} B scratch per lane, {launch['lds_bytes']} B LDS")
-        want = launch["grid"] * launch["block"] // 64
         if "SQ_WAVES" in c and int(round(c["SQ_WAVES"])) != want:
             res["rejected"] = (f"SQ_WAVES {c['SQ_WAVES']:.0f} != the launch's {want} waves: the counters describe another "
                                "launch shape")

@@ -120,3 +120,28 @@ def test_options_round_trip_and_reject_bad_values():
     assert e.value.status == hrt.ERR_INVALID_ARG
     with pytest.raises(TypeError):
         s.set_options(chunk_tail=3)
+
+
+def test_view_hint_places_only_and_clears():
+    """hrt_scene_set_view is a placement hint: it changes which node parts of random_10k's stream (beyond LDS)
+    are staged, NULL restores the default placement byte for byte, and it is refused after commit like every
+    other scene setting (the commit needs a device, so the refusal is checked on the uncommitted path)."""
+    def walk(s):
+        b, i = hrt.scene_blob(s)
+        return bytes(b)[i.off_walk:i.off_walk + i.walk_bytes], i.walk_hot
+
+    s0 = hrt.preset("random_10k", 1, None)
+    base, hot0 = walk(s0)
+    s1 = hrt.preset("random_10k", 1, None)
+    s1.set_view(hrt.preset_camera(s1.info, 3840, 2160))
+    viewed, hot1 = walk(s1)
+    assert hot0 == hot1 > 0 and viewed != base and len(viewed) == len(base)
+    s2 = hrt.preset("random_10k", 1, None)
+    s2.set_view(hrt.preset_camera(s2.info, 3840, 2160))
+    s2.set_view(None)
+    assert walk(s2)[0] == base
+    s3 = hrt.preset("random", 1, None)  # a stream staged whole: no placement choice to make
+    b3 = walk(s3)[0]
+    s3b = hrt.preset("random", 1, None)
+    s3b.set_view(hrt.preset_camera(s3b.info, 1920, 1080))
+    assert walk(s3b)[0] == b3

@@ -61,10 +61,12 @@ def sim_submuladd(tmp_path_factory):
 
 
 def sim_render(L, name, w, h, spp, depth, seed, earth, kernel, cull, region=None, sample_offset=0, t_min=0.001,
-               options=None):
+               options=None, view=False):
     s = hrt.preset(name, 1, earth, options=options)
-    blob, info = hrt.scene_blob(s)
     cam = hrt.preset_camera(s.info, w, h)
+    if view:
+        s.set_view(cam)
+    blob, info = hrt.scene_blob(s)
     p = hrt.params(w, h, spp, depth, seed, tuple(s.info.background), sample_offset=sample_offset, t_min=t_min)
     x0, y0, rw, rh = region if region is not None else (0, 0, w, h)
     out = np.zeros((rh, rw, 4), np.float32)
@@ -618,3 +620,25 @@ def test_c16_stream_renders_like_the_32b_stream(sim, earth, monkeypatch):
     ref, cnt = oracle_render("random_10k", 3840, 2160, 6, 50, 3, earth, region=region)
     assert sa["segments"] == cnt["segments"] and np.abs(a - ref).max() <= TOL
     print("node visits: 16-B parts", sa["nodes"], "32-B parts", sb["nodes"])
+
+
+@pytest.mark.parametrize("name,kernel,region", [("random_10k", 0, (1600, 900, 32, 8)), ("final", 3, (300, 420, 24, 8))])
+def test_view_placement_renders_the_same_frame(sim, earth, name, kernel, region):
+    """hrt_scene_set_view: a walk stream beyond LDS (random_10k's sphere stream, BASELINE
+    config 4; Final's general stream) stages the node parts the view's camera rays visit most instead of those
+    under the largest boxes.  Same hierarchy, other addresses: the stream's bytes differ, its size and staged
+    bytes do not, and the lane renders the same pixels bit for bit with the same rays and node visits."""
+    W, H, spp = (3840, 2160, 4) if name == "random_10k" else (800, 800, 4)
+    s0 = hrt.preset(name, 1, earth)
+    b0, i0 = hrt.scene_blob(s0)
+    s1 = hrt.preset(name, 1, earth)
+    s1.set_view(hrt.preset_camera(s1.info, W, H))
+    b1, i1 = hrt.scene_blob(s1)
+    assert i0.walk_hot > 0 and (i0.walk_hot, i0.walk_bytes) == (i1.walk_hot, i1.walk_bytes)
+    w0 = bytes(b0)[i0.off_walk:i0.off_walk + i0.walk_bytes]
+    w1 = bytes(b1)[i1.off_walk:i1.off_walk + i1.walk_bytes]
+    assert w0 != w1 and w0[:32] == w1[:32]  # the root stays first
+    a, sa = sim_render(sim, name, W, H, spp, 50, 3, earth, kernel=kernel, cull=CULL_EXACT, region=region)
+    b, sb = sim_render(sim, name, W, H, spp, 50, 3, earth, kernel=kernel, cull=CULL_EXACT, region=region, view=True)
+    assert (sa["segments"], sa["nodes"], sa["prims"]) == (sb["segments"], sb["nodes"], sb["prims"])
+    assert np.array_equal(a, b)
