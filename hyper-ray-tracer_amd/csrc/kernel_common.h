@@ -90,7 +90,7 @@ __device__ __forceinline__ void stage_scene(const KParams& P, float4* lds, const
 }
 
 /* A lane's current work item: one pixel and a chunk [sample, sample_end) of its samples.  slot: where
- * the chunk's result goes, P.out[slot] (one chunk) or P.partial[slot] = [n_out][chunk] (the host checks
+ * the chunk's result goes, P.out[slot] (one chunk) or P.partial[slot] = [chunk][n_out] (the host checks
  * n_chunks x n_out < 2^32); the chunk is first iff sample_end <= P.chunk (lane.h chunk_plan). */
 struct Item {
   uint32_t pxy; /* px | py << 16 */
@@ -191,7 +191,7 @@ __device__ __forceinline__ void claim_work(const KParams& P, uint32_t lane, bool
   if (lx < T.w && ly < T.h) {
     has_item = true;
     it.pxy = (T.x + lx) | ((T.y + ly) << 16);
-    it.slot = (T.out_off + ly * T.w + lx) * P.n_chunks + c;
+    it.slot = c * P.n_out + (T.out_off + ly * T.w + lx);
     chunk_range(P, c, it.sample, it.sample_end);
   }
 }

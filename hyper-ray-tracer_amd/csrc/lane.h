@@ -77,7 +77,9 @@ struct KParams {
   uint32_t walk_cap;   /* watchdog: more consecutive walk-loop iterations than any valid walk needs */
   uint32_t motion_uniform; /* every moving sphere has time0 = motion_t0, time1 - time0 = motion_span */
   float motion_t0, motion_span;
-  float4* partial; /* [n_out][n_chunks] chunk sums (n_chunks > 1): a pixel's chunks share cache lines */
+  float4* partial; /* [n_chunks][n_out] chunk sums (n_chunks > 1): a claim's 64 lanes write one chunk of 64
+                      consecutive pixels, whole cache lines (r05; [n_out][n_chunks] wrote 2.35x the sums' bytes
+                      on Final, 16-B writes into lines a wave completes only chunks later) */
   /* sphere-scene walk stream (layout.h; render_basic_kernel under CULL_EXACT) */
   const uint8_t* walk;
   uint32_t walk_bytes; /* whole stream */

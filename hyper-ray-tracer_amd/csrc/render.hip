@@ -240,10 +240,10 @@ __global__ __launch_bounds__(256) void reduce_chunks(const float4* __restrict__ 
                                                      uint32_t n_out, uint32_t n_chunks, uint32_t spp) {
   const float scale = 1.0f / (float)spp;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_out; i += gridDim.x * blockDim.x) {
-    float4 a = partial[(size_t)i * n_chunks];
+    float4 a = partial[i];
     Vec3 sum = v3(a.x, a.y, a.z);
     for (uint32_t c = 1; c < n_chunks; c++) {
-      float4 b = partial[(size_t)i * n_chunks + c];
+      float4 b = partial[(size_t)c * n_out + i];
       sum = sum + v3(b.x, b.y, b.z);
     }
     out[i] = make_float4(sqrtf(sum.x * scale), sqrtf(sum.y * scale), sqrtf(sum.z * scale), 1.0f);

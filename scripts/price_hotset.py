@@ -144,6 +144,52 @@ def main():
     lds = v_te[hot].sum() / len(te)
     print(f"  proxy: camera rays to the nearest leaf box ({len(pr)} rays): in LDS {lds:.2f}, global {per_ray - lds:.2f}",
           flush=True)
+    # + one bounce off the entered leaf box: from the entry point, a random direction about the entered face's normal
+    hit = np.isfinite(tb)
+    ob = o[hit] + tb[hit, None] * d[hit]
+    ib = inv[hit]
+    # the entered face: the axis whose slab entry is the latest
+    lbh = None
+    nrm = np.zeros_like(ob)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        best = np.full(len(ob), -1)
+        tbest = np.full(len(ob), np.inf)
+        for c0 in range(0, len(lb), 256):
+            bx = lb[c0:c0 + 256]
+            t0 = (bx[None, :, :3] - o[hit][:, None, :]) * ib[:, None, :]
+            t1 = (bx[None, :, 3:] - o[hit][:, None, :]) * ib[:, None, :]
+            lo = np.maximum(np.nanmax(np.minimum(t0, t1), axis=2), 0.001)
+            hi = np.nanmin(np.maximum(t0, t1), axis=2)
+            t = np.where(lo <= hi, lo, np.inf)
+            k = t.argmin(axis=1)
+            tk = t[np.arange(len(ob)), k]
+            bet = tk < tbest
+            tbest[bet], best[bet] = tk[bet], c0 + k[bet]
+        bx = lb[best]
+        t0 = (bx[:, :3] - o[hit]) * ib
+        t1 = (bx[:, 3:] - o[hit]) * ib
+        ax = np.nanargmax(np.minimum(t0, t1), axis=1)
+    nrm[np.arange(len(ob)), ax] = -np.sign(d[hit][np.arange(len(ob)), ax])
+    g = rng.normal(size=ob.shape)
+    db = nrm + g / np.linalg.norm(g, axis=1, keepdims=True)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ibb = 1.0 / db
+        tb2 = np.full(len(ob), np.inf)
+        for c0 in range(0, len(lb), 256):
+            bx = lb[c0:c0 + 256]
+            t0 = (bx[None, :, :3] - ob[:, None, :]) * ibb[:, None, :]
+            t1 = (bx[None, :, 3:] - ob[:, None, :]) * ibb[:, None, :]
+            lo = np.maximum(np.nanmax(np.minimum(t0, t1), axis=2), 0.01)
+            hi = np.nanmin(np.maximum(t0, t1), axis=2)
+            t = np.where(lo <= hi, lo, np.inf)
+            tb2 = np.minimum(tb2, t.min(axis=1))
+    pr2 = np.concatenate([pr, np.c_[ob, db, tb2].astype(np.float32)])
+    v_pr = visits(boxes, parent, pr2).sum(axis=1)
+    hot = np.zeros(len(offs), bool)
+    hot[np.argsort(-v_pr, kind="stable")[:n_hot_parts]] = True
+    lds = v_te[hot].sum() / len(te)
+    print(f"  proxy: leaf-box camera rays + one bounce off the entered face ({len(pr2)} rays): in LDS {lds:.2f}, "
+          f"global {per_ray - lds:.2f}", flush=True)
     for nr in (1000, 4000):
         v_pr = visits(boxes, parent, pr[:nr]).sum(axis=1)
         hot = np.zeros(len(offs), bool)
