@@ -529,6 +529,7 @@ def main():
             torch.distributed.barrier()
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    switch = torch.zeros(1, device=dev)
     barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -536,6 +537,11 @@ def main():
         if turns:  # --one-device rehearsal: rank r launches its share while the others wait at the barrier
             for r in range(world):
                 if r == rank:
+                    # the GPU switching to this process's queue (up to ~25 ms after the other rank's turn, r05 kernel
+                    # traces) happens on a one-element fill before the clock starts: separate GPUs do not pay it
+                    with torch.cuda.stream(stream):
+                        switch.zero_()
+                    torch.cuda.synchronize(dev)
                     ev[k][0].record(stream)
                     hrt.render_tiles_device(scene, cam, p, tiles, out.data_ptr(), stream.cuda_stream)
                     ev[k][1].record(stream)

@@ -92,10 +92,11 @@ step() {
       local rc=$?; echo "== $tag exit $rc" >> "$LOG"; return $rc ;;
     configs)
       local tag=$1
-      # C3 with its parity rows and CPU baseline; C4's whole frame without (one 4K row at 2000 spp is ~70 s of the
-      # oracle's reference culling); C4's and C5's 1/8 shares with parity tiles and a CPU baseline on tiles
+      # C3 with its parity rows and CPU baseline; C4's whole frame with the fewest rows the CPU budget allows (a 4K
+      # row at 2000 spp is ~20 s of the oracle's reference culling on 16 threads); C4's and C5's 1/8 shares with
+      # parity tiles and a CPU baseline on tiles
       bench_line "${tag}_configs" 300 --steps 1 --warmup 1 --no-delivery --preset earth_perlin --spp 1000 && \
-      bench_line "${tag}_configs" 400 --steps 1 --warmup 1 --no-cpu-baseline --no-delivery --preset random_10k --width 3840 --height 2160 --spp 2000 && \
+      bench_line "${tag}_configs" 500 --steps 1 --warmup 1 --no-delivery --preset random_10k --width 3840 --height 2160 --spp 2000 && \
       bench_line "${tag}_configs" 300 --steps 1 --warmup 1 --no-delivery --preset random_10k --width 3840 --height 2160 --spp 2000 --share 8 && \
       bench_line "${tag}_configs" 300 --steps 1 --warmup 1 --no-delivery --preset cornell --width 2048 --height 2048 --spp 10000 --share 8 ;;
     profile) profile "$@" ;;
