@@ -591,12 +591,64 @@ Aabb box_union(const Aabb& a, const Aabb& b) {
   return u;
 }
 
+/* ---- hrt_scene_set_view: what the hierarchy builders use of the view (performance only: any hierarchy over
+ * the reference leaf order, placed anywhere, renders the same image, DESIGN.md sections 4-5) */
+/* f64 slab test of b on [lo, hi]; an axis whose product is NaN (0 x inf: the origin on a slab plane) is skipped.
+ * On a hit, *entry = the entry t.  For nested boxes the outcome is monotone (a superset passes whenever a
+ * subset does: rounding is monotone). */
+static bool view_slab(const Aabb& b, const double* o, const double* inv, double lo, double hi, double* entry = nullptr) {
+  for (int k = 0; k < 3; k++) {
+    const double t0 = (b.mn[k] - o[k]) * inv[k], t1 = (b.mx[k] - o[k]) * inv[k];
+    const double a = std::min(t0, t1), c = std::max(t0, t1);
+    if (a == a) lo = std::max(lo, a);
+    if (c == c) hi = std::min(hi, c);
+  }
+  if (entry) *entry = lo;
+  return lo <= hi;
+}
+/* a pinhole camera ray through (u, v) of the view's image plane (lens and shutter ignored) */
+static void view_ray(const hrt_camera& c, double u, double v, double* o, double* inv) {
+  for (int k = 0; k < 3; k++) {
+    o[k] = c.origin[k];
+    inv[k] = 1.0 / ((double)c.lower_left_corner[k] + u * c.horizontal[k] + v * c.vertical[k] - o[k]);
+  }
+}
+constexpr double VIEW_TMIN = 0.001;
+/* camera rays through a VIEW_DP_GRID x VIEW_DP_GRID grid, each stopped at the nearest leaf box it enters (a
+ * stand-in for its closest hit that needs no primitive code) */
+constexpr uint32_t VIEW_DP_GRID = 64;
+struct ViewRays {
+  std::vector<double> o, inv, cl;
+  uint32_t n = 0;
+};
+static ViewRays view_rays(const hrt_camera& c, const std::vector<WalkLeaf>& leaves) {
+  ViewRays R;
+  R.n = VIEW_DP_GRID * VIEW_DP_GRID;
+  R.o.resize(3 * (size_t)R.n);
+  R.inv.resize(3 * (size_t)R.n);
+  R.cl.assign(R.n, HUGE_VAL);
+  for (uint32_t q = 0; q < R.n; q++) {
+    view_ray(c, (q % VIEW_DP_GRID + 0.5) / VIEW_DP_GRID, (q / VIEW_DP_GRID + 0.5) / VIEW_DP_GRID, &R.o[3 * q], &R.inv[3 * q]);
+    for (const WalkLeaf& L : leaves) {
+      double t;
+      if (view_slab(L.box, &R.o[3 * q], &R.inv[3 * q], VIEW_TMIN, R.cl[q], &t)) R.cl[q] = t;
+    }
+  }
+  return R;
+}
+/* the share of the re-grouping DP's node cost given to the view's rays (the rest: surface area, for the
+ * scattered rays; priced flat between 0.35 and 0.6 on C2, scripts/price_hierarchy.py) */
+constexpr double VIEW_DP_MIX = 0.5;
+
 /* Optimal re-grouping of a fixed leaf sequence by dynamic programming (HRT_WALK_DP = 1 | 2, n <= 2048):
  * cost(i, j) = w(i, j) + min_k cost(i, k) + cost(k, j) over the ranges of the sequence, with w = 2 x the half
  * area (mode 1: the two child tests an inner node makes whenever a ray passes it) or half area x leaves
  * (mode 2: walk_regroup's greedy objective, minimised exactly).  Splits tie to the cut nearest the middle. */
+/* With view rays (hrt_scene_set_view, mode 1): w(i, j) = 2 x (VIEW_DP_MIX x the share of the view's rays whose
+ * slab test of the range's box passes before their closest + (1 - VIEW_DP_MIX) x half area / area_root). */
 bool walk_regroup_dp(std::vector<WNode>& T, const std::vector<WalkLeaf>& all, int mode, uint32_t lo0 = 0,
-                     uint32_t hi0 = 0xFFFFFFFFu, uint32_t depth0 = 0) {
+                     uint32_t hi0 = 0xFFFFFFFFu, uint32_t depth0 = 0, const ViewRays* vr = nullptr,
+                     double area_root = 0.0) {
   /* over the leaves [lo0, hi0) (default: all), the subtree's nodes appended to T at depth depth0 */
   if (hi0 > all.size()) hi0 = (uint32_t)all.size();
   const WalkLeaf* leaves = all.data() + lo0;
@@ -616,6 +668,36 @@ bool walk_regroup_dp(std::vector<WNode>& T, const std::vector<WalkLeaf>& all, in
       A[at(i, j)] = half_area(u);
     }
   }
+  std::vector<double> P;
+  const bool view = vr != nullptr && mode == 1 && area_root > 0.0;
+  if (view) {
+    /* per start i, each ray's first end j whose box it passes (monotone in j: nested boxes), by bisection */
+    P.assign((size_t)n * (n + 1), 0.0);
+    std::vector<uint32_t> rs;
+    for (uint32_t q = 0; q < vr->n; q++)
+      if (view_slab(box[at(0, n)], &vr->o[3 * q], &vr->inv[3 * q], VIEW_TMIN, vr->cl[q])) rs.push_back(q);
+    std::vector<uint32_t> first(n + 2);
+    for (uint32_t i = 0; i < n; i++) {
+      std::fill(first.begin(), first.end(), 0u);
+      for (uint32_t q : rs) {
+        const double* o = &vr->o[3 * q];
+        const double* iv = &vr->inv[3 * q];
+        if (!view_slab(box[at(i, n)], o, iv, VIEW_TMIN, vr->cl[q])) continue;
+        uint32_t a = i + 1, b = n; /* the smallest j in [a, b] that passes: b does */
+        while (a < b) {
+          const uint32_t m = a + (b - a) / 2;
+          if (view_slab(box[at(i, m)], o, iv, VIEW_TMIN, vr->cl[q])) b = m;
+          else a = m + 1;
+        }
+        first[a]++;
+      }
+      uint32_t c = 0;
+      for (uint32_t j = i + 1; j <= n; j++) {
+        c += first[j];
+        P[at(i, j)] = (double)c / vr->n;
+      }
+    }
+  }
   for (uint32_t len = 2; len <= n; len++)
     for (uint32_t i = 0; i + len <= n; i++) {
       const uint32_t j = i + len, mid = i + len / 2;
@@ -629,7 +711,9 @@ bool walk_regroup_dp(std::vector<WNode>& T, const std::vector<WalkLeaf>& all, in
           bk = k;
         }
       }
-      C[at(i, j)] = best + (mode == 2 ? A[at(i, j)] * len : 2.0 * A[at(i, j)]);
+      C[at(i, j)] = best + (mode == 2 ? A[at(i, j)] * len
+                                      : view ? 2.0 * (VIEW_DP_MIX * P[at(i, j)] + (1.0 - VIEW_DP_MIX) * A[at(i, j)] / area_root)
+                                             : 2.0 * A[at(i, j)]);
       K[at(i, j)] = bk;
     }
   struct Range { uint32_t lo, hi, depth; };
@@ -651,12 +735,24 @@ bool walk_regroup_dp(std::vector<WNode>& T, const std::vector<WalkLeaf>& all, in
 }
 
 /* re-grouped hierarchy over leaves[0, n), iterative, pre-order (a range of n leaves is 2n - 1 nodes) */
-void walk_regroup(std::vector<WNode>& T, const std::vector<WalkLeaf>& leaves) {
+void walk_regroup(std::vector<WNode>& T, const std::vector<WalkLeaf>& leaves, const hrt_camera* view = nullptr) {
   /* default: the DP (mode 1) for sequences of at most 700 leaves (O(n^3 / 6) work: ~30 ms at Random's 485),
-   * the greedy split above that (and on the device, build_walk.hip) */
+   * the greedy split above that (and on the device, build_walk.hip).  With a view (hrt_scene_set_view) the
+   * DP's node cost mixes in the view's camera rays (walk_regroup_dp); leaves without a box keep it off. */
   const char* dp = knob_env("HRT_WALK_DP");
   const int mode = dp ? dp[0] - '0' : (leaves.size() <= 700 ? 1 : 3);
-  if ((mode == 1 || mode == 2) && walk_regroup_dp(T, leaves, mode)) return;
+  ViewRays vr;
+  double area_root = 0.0;
+  bool boxes = !leaves.empty();
+  for (const WalkLeaf& L : leaves) boxes = boxes && !L.nobox;
+  if (view && boxes) {
+    vr = view_rays(*view, leaves);
+    Aabb u = leaves[0].box;
+    for (const WalkLeaf& L : leaves) u = box_union(u, L.box);
+    area_root = half_area(u);
+  }
+  const ViewRays* vp = area_root > 0.0 ? &vr : nullptr;
+  if ((mode == 1 || mode == 2) && walk_regroup_dp(T, leaves, mode, 0, 0xFFFFFFFFu, 0, vp, area_root)) return;
   /* mode 3 (default above 700 leaves): the greedy split below, and each range of at most DP_SUB leaves it
    * reaches re-grouped by the DP (mode 1) */
   const char* ds = knob_env("HRT_WALK_DP_SUB");
@@ -672,7 +768,7 @@ void walk_regroup(std::vector<WNode>& T, const std::vector<WalkLeaf>& leaves) {
       T.push_back(WNode{leaves[r.lo].box, (int32_t)r.lo, self + 1, r.depth});
       continue;
     }
-    if (n <= dp_sub && walk_regroup_dp(T, leaves, 1, r.lo, r.hi, r.depth)) continue;
+    if (n <= dp_sub && walk_regroup_dp(T, leaves, 1, r.lo, r.hi, r.depth, vp, area_root)) continue;
     pre.resize(n);
     suf.resize(n);
     pre[0] = leaves[r.lo].box;
@@ -980,28 +1076,16 @@ constexpr uint32_t VIEW_GRID = 128;
 static std::vector<uint32_t> view_heat(const hrt_camera& c, const std::vector<WNode>& T) {
   const uint32_t N = (uint32_t)T.size();
   std::vector<uint32_t> heat(N, 0);
-  const double tmin = 0.001;
   for (uint32_t gy = 0; gy < VIEW_GRID; gy++)
     for (uint32_t gx = 0; gx < VIEW_GRID; gx++) {
-      const double u = (gx + 0.5) / VIEW_GRID, v = (gy + 0.5) / VIEW_GRID;
       double o[3], inv[3];
-      for (int k = 0; k < 3; k++) {
-        o[k] = c.origin[k];
-        const double d = (double)c.lower_left_corner[k] + u * c.horizontal[k] + v * c.vertical[k] - o[k];
-        inv[k] = 1.0 / d;
-      }
+      view_ray(c, (gx + 0.5) / VIEW_GRID, (gy + 0.5) / VIEW_GRID, o, inv);
       double closest = HUGE_VAL;
       for (uint32_t i = 0; i < N;) {
         heat[i]++;
-        double lo = tmin, hi = closest;
-        for (int k = 0; k < 3; k++) {
-          const double t0 = (T[i].box.mn[k] - o[k]) * inv[k], t1 = (T[i].box.mx[k] - o[k]) * inv[k];
-          const double a = std::min(t0, t1), b = std::max(t0, t1);
-          if (a == a) lo = std::max(lo, a); /* NaN (0 x inf: the origin on a slab plane) leaves the bound */
-          if (b == b) hi = std::min(hi, b);
-        }
-        if (lo <= hi) {
-          if (T[i].leaf >= 0) closest = std::min(closest, lo);
+        double t;
+        if (view_slab(T[i].box, o, inv, VIEW_TMIN, closest, &t)) {
+          if (T[i].leaf >= 0) closest = std::min(closest, t);
           i++;
         } else {
           i = T[i].end;
@@ -1671,7 +1755,7 @@ void build_walk(hrt_scene* s) {
     if (regroup_ok && s->opts.walk_tree == 0) {
       const auto t0 = std::chrono::steady_clock::now();
       T.clear();
-      walk_regroup(T, leaves);
+      walk_regroup(T, leaves, s->has_view ? &s->view : nullptr);
       s->w_build_us = (uint32_t)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
       s->w_regrouped = true;
     }
@@ -1691,7 +1775,7 @@ void build_walk(hrt_scene* s) {
       s->w_general = true;
       if (gok && s->opts.walk_tree == 0) {
         TG.clear();
-        walk_regroup(TG, gl);
+        walk_regroup(TG, gl, s->has_view ? &s->view : nullptr);
         s->w_regrouped = true;
       }
       walk_place_and_write(s, TG, gl);
@@ -1705,7 +1789,7 @@ void build_walk(hrt_scene* s) {
   else if (regroup) {
     const auto t0 = std::chrono::steady_clock::now();
     T.clear();
-    walk_regroup(T, leaves);
+    walk_regroup(T, leaves, s->has_view ? &s->view : nullptr);
     s->w_build_us = (uint32_t)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
     s->w_regrouped = true;
   }

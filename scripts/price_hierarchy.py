@@ -114,6 +114,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--preset", default="random")
     ap.add_argument("--rays", type=int, default=20000)
+    ap.add_argument("--grid", type=int, default=64, help="camera rays of the view proxy: grid x grid")
     a = ap.parse_args()
     L = build()
     L.lane_sim_segments.restype = ctypes.c_int
@@ -133,7 +134,32 @@ def main():
     K_p = dp(Ptr)
     r_sa, r_p = inner_ranges(K_sa, n), inner_ranges(K_p, n)
     print(f"expected node visits per segment (final closest, test rays): surface-area DP {visits(Pte, r_sa):.2f}, "
-          f"ray-probability DP {visits(Pte, r_p):.2f} (in-sample {visits(Ptr, r_p):.2f})")
+          f"ray-probability DP {visits(Pte, r_p):.2f} (in-sample {visits(Ptr, r_p):.2f})", flush=True)
+    # what a commit with hrt_scene_set_view could compute: pinhole camera rays stopped at the nearest leaf box,
+    # mixed with the surface-area term for the secondary rays (their share of the segments: 1 - 1 / rays per sample)
+    cam = hrt.preset_camera(s.info, 1920, 1080)
+    g = (np.arange(a.grid) + 0.5) / a.grid
+    u, v = np.meshgrid(g, g)
+    u, v = u.ravel(), v.ravel()
+    org = np.array(cam.origin, np.float64)
+    d = (np.array(cam.lower_left_corner) + u[:, None] * np.array(cam.horizontal) + v[:, None] * np.array(cam.vertical)) - org
+    o = np.tile(org, (len(d), 1))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        inv = 1.0 / d
+        t0 = (boxes[None, :, :3] - o[:, None, :]) * inv[:, None, :]
+        t1 = (boxes[None, :, 3:] - o[:, None, :]) * inv[:, None, :]
+        lo = np.maximum(np.nanmax(np.minimum(t0, t1), axis=2), 0.001)
+        hi = np.nanmin(np.maximum(t0, t1), axis=2)
+        tb = np.where(lo <= hi, lo, np.inf).min(axis=1)
+    cam_rays = np.c_[o, d, np.where(np.isfinite(tb), tb, 3.0e38)].astype(np.float32)
+    Pcam = range_prob(L, boxes, cam_rays)
+    A = half_areas(boxes)
+    f1 = 1.0 / 2.83
+    for lam in (0.0, f1, 0.6, 1.0):
+        Wmix = lam * Pcam + (1 - lam) * A / A[0, n]
+        r_m = inner_ranges(dp(Wmix), n)
+        print(f"  view proxy (camera rays to the nearest leaf box) x {lam:.2f} + surface area x {1 - lam:.2f}: "
+              f"{visits(Pte, r_m):.2f}", flush=True)
 
 
 if __name__ == "__main__":

@@ -140,8 +140,15 @@ def test_view_hint_places_only_and_clears():
     s2.set_view(hrt.preset_camera(s2.info, 3840, 2160))
     s2.set_view(None)
     assert walk(s2)[0] == base
-    s3 = hrt.preset("random", 1, None)  # a stream staged whole: no placement choice to make
-    b3 = walk(s3)[0]
+    # a stream staged whole (Random) has no placement choice; its re-grouped hierarchy does weigh the view's rays
+    # (walk_regroup_dp), and with the reference tree itself (walk_tree 1) the view changes nothing
+    s3 = hrt.preset("random", 1, None)
+    b3, h3 = walk(s3)
     s3b = hrt.preset("random", 1, None)
     s3b.set_view(hrt.preset_camera(s3b.info, 1920, 1080))
-    assert walk(s3b)[0] == b3
+    b3b, h3b = walk(s3b)
+    assert h3 == h3b == 0 and len(b3b) == len(b3) and b3b != b3
+    t0 = hrt.preset("random", 1, None, options={"walk_tree": 1})
+    t1 = hrt.preset("random", 1, None, options={"walk_tree": 1})
+    t1.set_view(hrt.preset_camera(t1.info, 1920, 1080))
+    assert walk(t0)[0] == walk(t1)[0]

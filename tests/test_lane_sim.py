@@ -622,23 +622,31 @@ def test_c16_stream_renders_like_the_32b_stream(sim, earth, monkeypatch):
     print("node visits: 16-B parts", sa["nodes"], "32-B parts", sb["nodes"])
 
 
-@pytest.mark.parametrize("name,kernel,region", [("random_10k", 0, (1600, 900, 32, 8)), ("final", 3, (300, 420, 24, 8))])
+@pytest.mark.parametrize("name,kernel,region", [("random_10k", 0, (1600, 900, 32, 8)), ("final", 3, (300, 420, 24, 8)),
+                                                ("random", 0, (700, 500, 48, 8))])
 def test_view_placement_renders_the_same_frame(sim, earth, name, kernel, region):
-    """hrt_scene_set_view: a walk stream beyond LDS (random_10k's sphere stream, BASELINE
-    config 4; Final's general stream) stages the node parts the view's camera rays visit most instead of those
-    under the largest boxes.  Same hierarchy, other addresses: the stream's bytes differ, its size and staged
-    bytes do not, and the lane renders the same pixels bit for bit with the same rays and node visits."""
-    W, H, spp = (3840, 2160, 4) if name == "random_10k" else (800, 800, 4)
+    """hrt_scene_set_view (DESIGN.md sections 4-5): the re-grouping DP weighs the view's camera rays (Random,
+    random_10k: another hierarchy over the same leaf order, fewer node visits) and a walk stream beyond LDS
+    (random_10k's sphere stream, BASELINE config 4; Final's general stream) stages the node parts those rays
+    visit most.  The stream's bytes differ, its size and staged bytes do not, and the lane renders the same
+    pixels bit for bit with the same rays and primitive tests (and, where only the placement moved, the same
+    node visits)."""
+    W, H, spp = {"random_10k": (3840, 2160, 4), "final": (800, 800, 4), "random": (1920, 1080, 8)}[name]
     s0 = hrt.preset(name, 1, earth)
     b0, i0 = hrt.scene_blob(s0)
     s1 = hrt.preset(name, 1, earth)
     s1.set_view(hrt.preset_camera(s1.info, W, H))
     b1, i1 = hrt.scene_blob(s1)
-    assert i0.walk_hot > 0 and (i0.walk_hot, i0.walk_bytes) == (i1.walk_hot, i1.walk_bytes)
+    assert (i0.walk_hot > 0) == (name != "random") and (i0.walk_hot, i0.walk_bytes) == (i1.walk_hot, i1.walk_bytes)
     w0 = bytes(b0)[i0.off_walk:i0.off_walk + i0.walk_bytes]
     w1 = bytes(b1)[i1.off_walk:i1.off_walk + i1.walk_bytes]
-    assert w0 != w1 and w0[:32] == w1[:32]  # the root stays first
+    assert w0 != w1
     a, sa = sim_render(sim, name, W, H, spp, 50, 3, earth, kernel=kernel, cull=CULL_EXACT, region=region)
     b, sb = sim_render(sim, name, W, H, spp, 50, 3, earth, kernel=kernel, cull=CULL_EXACT, region=region, view=True)
-    assert (sa["segments"], sa["nodes"], sa["prims"]) == (sb["segments"], sb["nodes"], sb["prims"])
+    assert (sa["segments"], sa["prims"]) == (sb["segments"], sb["prims"])
+    if name == "final":  # its general stream keeps its hierarchy (a leaf without a box turns the view DP off)
+        assert sa["nodes"] == sb["nodes"]
+    else:
+        assert sb["nodes"] < sa["nodes"], (sa["nodes"], sb["nodes"])
     assert np.array_equal(a, b)
+    print(name, "node visits", sa["nodes"], "->", sb["nodes"])
