@@ -94,6 +94,10 @@ def parse():
                     help="--one-device timing: ranks launch their shares in turns (each launch alone on the GPU, "
                          "as on separate GPUs), or all at once (the ranks' persistent grids then contend for the "
                          "one GPU, DESIGN.md section 9)")
+    ap.add_argument("--streams", default="auto",
+                    help="timed steps round-robin over this many HIP streams (their own output buffers and library "
+                         "slots): a step's persistent grid then starts on the CUs the previous step's last waves free.  "
+                         "'auto' = 2 for a short launch of a tile share (stream_count), else 1")
     ap.add_argument("--allow-knobs", action="store_true",
                     help="print the line even when A/B environment knobs of the library are set (never for a headline)")
     ap.add_argument("--chunks", choices=["auto", "frame"], default="auto",
@@ -159,6 +163,7 @@ def distinct_devices(devices):
 
 
 SHORT_LAUNCH_SAMPLES = 500e6  # below this many samples per GPU a launch's end is a visible part of it
+OVERLAP_LAUNCH_SAMPLES = 600e6  # stream_count: C2's halves (518 M samples) still gain from overlapping steps
 
 
 def chunk_options(args, share):
@@ -170,6 +175,16 @@ def chunk_options(args, share):
     if args.chunks == "auto" and share >= 4 and args.width * args.height * args.spp / share < SHORT_LAUNCH_SAMPLES:
         return {"chunk_min": 8, "chunk_max": 64}
     return None
+
+
+def stream_count(args, share):
+    """--streams: how many HIP streams the timed steps alternate over.  Two for a GPU's share of a tile split in a
+    short launch (under OVERLAP_LAUNCH_SAMPLES: C2's shares), so the next step's grid fills the CUs the end of the
+    previous one frees (profiles/r05_stream_overlap_ab.jsonl: C2's 1/8 share +5.5%, 1/4 +1%, 1/2 +1.6%); one for a
+    whole frame (within noise, and once 3.5% slower) and for long launches (C4's 1/8 share: 3.3% slower)."""
+    if args.streams != "auto":
+        return max(1, int(args.streams))
+    return 2 if share >= 2 and args.width * args.height * args.spp / share < OVERLAP_LAUNCH_SAMPLES else 1
 
 
 def knob_report(launch):
@@ -519,10 +534,13 @@ def main():
     warm_s = time.perf_counter() - tw
     progress = warm_s > 20.0  # long frames: a progress line per timed frame
     log(f"work-count frame: {seg_step} rays in {warm_s:.1f} s")
+    n_str = 1 if turns else stream_count(args, share_of)
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(n_str - 1)]
+    outs = [out] + [torch.empty_like(out) for _ in range(n_str - 1)]
     # W warm-up steps as the timed ones run them (asynchronous launches: the first one also sizes the
     # library's other in-flight slots, so no timed step allocates device or pinned memory)
-    for _ in range(max(1, args.warmup)):
-        hrt.render_tiles_device(scene, cam, p, tiles, out.data_ptr(), stream.cuda_stream)
+    for k in range(max(n_str, args.warmup)):
+        hrt.render_tiles_device(scene, cam, p, tiles, outs[k % n_str].data_ptr(), streams[k % n_str].cuda_stream)
 
     def barrier():
         if world > 1:
@@ -548,9 +566,10 @@ def main():
                     torch.cuda.synchronize(dev)
                 barrier()
             continue
-        ev[k][0].record(stream)
-        hrt.render_tiles_device(scene, cam, p, tiles, out.data_ptr(), stream.cuda_stream)
-        ev[k][1].record(stream)
+        sk = streams[k % n_str]
+        ev[k][0].record(sk)
+        hrt.render_tiles_device(scene, cam, p, tiles, outs[k % n_str].data_ptr(), sk.cuda_stream)
+        ev[k][1].record(sk)
         if progress and k + 1 < args.steps:
             ev[k][1].synchronize()  # progress line per frame (long configs); the clock keeps running
             log(f"timed frame {k + 1}/{args.steps}")
@@ -569,6 +588,8 @@ def main():
             json.dump(launch, fh)
     log(f"timed steps done: {dt / args.steps * 1e3:.1f} ms per step", all_ranks=True)
     launch_ms = sum(a.elapsed_time(b) for a, b in ev) / max(1, args.steps)
+    if n_str > 1:  # overlapping steps: an event pair also spans the wait for the CUs; the step's share of the clock
+        launch_ms = dt / max(1, args.steps) * 1e3
     rank_ms = [round(launch_ms, 2)]
     if world > 1:
         import torch.distributed as dist
@@ -670,6 +691,7 @@ def main():
             "n_gpus": distinct_devices(devices),
             "steps": args.steps,
             "warmup": args.warmup,
+            "streams": n_str,
             "ms_per_step": round(dt / args.steps * 1e3, 2),
             "higher_is_better": True,
             "scaling": "strong" if tiled else "weak",  # tiles: the frame is the fixed total at every N

@@ -76,3 +76,15 @@ def test_share_tiles_for_the_cpu_leg_spread_in_two_dimensions():
         assert len(xs) >= want_x and len(ys) >= want_y, (W, H, world, rank, sorted(xs), sorted(ys))
         span_x = max(xs) - min(xs)
         assert len(picks) < 4 or span_x >= W / 2, (W, span_x)
+
+
+def test_stream_count_per_run():
+    """--streams auto: two alternating streams for a GPU's share of C2 (short launches: the next step's grid fills
+    the CUs the previous one's end frees), one for the whole frame and for C4's / C5's long share launches."""
+    def args(w, h, spp, streams="auto"):
+        return argparse.Namespace(width=w, height=h, spp=spp, streams=streams)
+    assert bench.stream_count(args(1920, 1080, 500), 1) == 1
+    assert [bench.stream_count(args(1920, 1080, 500), n) for n in (2, 4, 8)] == [2, 2, 2]
+    assert bench.stream_count(args(3840, 2160, 2000), 8) == 1
+    assert bench.stream_count(args(2048, 2048, 10000), 8) == 1
+    assert bench.stream_count(args(1920, 1080, 500, "3"), 1) == 3
