@@ -1491,12 +1491,16 @@ HRT_LANE_FI bool box_ce(const float4& a, const float4& b, const TRay& r, float t
   return !(hi < lo);
 }
 
-/* One node step: an inner node moves to pass / skip; a passed leaf parks the lane on it (WALK_PEND). */
+/* One node step: an inner node moves to pass / skip; a passed leaf parks the lane on it (WALK_PEND).  ls (the
+ * walk kernels, HRT_KEEP_SKIP): the step's skip link, kept in a register of the lane's own.  A leaf's skip IS its
+ * pre-order successor (layout.h), so a lane parked on a leaf continues there without reading the payload: in a
+ * hybrid stream every payload is a global read, one dependent L2 round trip per leaf in the walk loop. */
 /* FMA: box_ce's fused form (default except for the latency-bound hybrid walk; the sphere kernel's
  * HEAVY instantiation passes false: at its 128-VGPR cap the three more live registers cost 3% on C3) */
 template <bool COUNT, int MEM, bool FMA = HRT_BOX_FMA && (MEM != WM_HYB || HRT_BOX_FMA_ALL), bool NANG = true,
           uint32_t HALF = 16, bool C16 = false>
-HRT_LANE_FI void walk_box(const WalkSrc& src, uint32_t& i, const TRay& r, float tmin, float closest, Counts& cn) {
+HRT_LANE_FI void walk_box(const WalkSrc& src, uint32_t& i, const TRay& r, float tmin, float closest, Counts& cn,
+                          uint32_t* ls = nullptr) {
   if constexpr (C16) { /* layout.h WALK_C16: position = node index, part at 16 i */
     const float4 q = wload_part16<MEM>(src, i << 4);
     const uint32_t w0 = f2u(q.x), w1 = f2u(q.y), w2 = f2u(q.z);
@@ -1507,6 +1511,7 @@ HRT_LANE_FI void walk_box(const WalkSrc& src, uint32_t& i, const TRay& r, float 
     const float4 a = make_float4(h2f(w0 & 0xFFFFu), h2f(w0 >> 16), h2f(w1 & 0xFFFFu), 0.0f);
     const float4 b = make_float4(h2f(w1 >> 16), h2f(w2 & 0xFFFFu), h2f(w2 >> 16), 0.0f);
     if constexpr (COUNT) cn.nodes++;
+    if (ls) *ls = links & 0xFFFFu;
     i = box_ce<FMA, NANG>(a, b, r, tmin, closest) ? links >> 16 : links & 0xFFFFu;
     return;
   }
@@ -1520,6 +1525,7 @@ HRT_LANE_FI void walk_box(const WalkSrc& src, uint32_t& i, const TRay& r, float 
 #endif
 #endif
   if constexpr (COUNT) cn.nodes++;
+  if (ls) *ls = skip;
   i = box_ce<FMA, NANG>(a, b, r, tmin, closest) ? f2u(b.w) : skip;
 }
 

@@ -190,7 +190,9 @@ constexpr uint32_t KIND_MASK = 0x7Fu;
  * records may be placed anywhere: skip = the node that follows the subtree in pre-order (or the end
  * offset); pass = the first child for an inner node, and (payload | WALK_PEND) for a leaf: the lane
  * parks on the leaf until the wave runs its primitive test (walk_prim), which continues at the
- * successor kept in w = WL_* flags | successor << 2.  The walk's winner is the payload's offset.  A leaf
+ * successor kept in w = WL_* flags | successor << 2.  A leaf's skip equals that successor (the next node in
+ * pre-order after a one-node subtree; tests/test_lane_sim.py checks every stream), so the walk kernels continue
+ * a parked lane at the skip they kept from the leaf's step (lane.h walk_box, HRT_KEEP_SKIP).  The walk's winner is the payload's offset.  A leaf
  * without a reference box (a List member: K_PRIM) has C = 0, E = +inf (the inflated test always
  * passes) and WL_NOBOX (no reference test).
  * Placement (scene.cpp walk_place_and_write): a stream within LDS_SCENE_MAX_BYTES is laid out in

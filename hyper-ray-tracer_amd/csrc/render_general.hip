@@ -29,6 +29,10 @@ using namespace hrt::kern;
 namespace {
 
 constexpr int GWALK_WAVES = HRT_GWALK_WAVES;
+#ifndef HRT_GWALK_KEEP_SKIP
+#define HRT_GWALK_KEEP_SKIP 1 /* hybrid streams: a parked lane continues at the skip kept from its leaf's step (lane.h
+                                 walk_box) instead of the successor read from the payload in global memory */
+#endif
 #ifndef HRT_GWALK_RECOMPUTE
 #define HRT_GWALK_RECOMPUTE 1 /* kernel_common.h claim_work<RECOMPUTE> */
 #endif
@@ -114,6 +118,8 @@ void render_gwalk_kernel(KParams P) {
   TRay r;
   set_ray(r, ps.ro, ps.rd, 0.0f, P);
   uint32_t node = G::NONE, winner = G::NONE, pend = G::NONE;
+  constexpr bool KEEP_SKIP = HRT_GWALK_KEEP_SKIP != 0 && WMEM == WM_HYB;
+  uint32_t nskip = G::NONE; /* KEEP_SKIP: the skip link of the lane's last node step */
   uint32_t gstate = G::NONE; /* the last leaf group whose box this walk tested, and its outcome (bit 31) */
   float closest = inf;
   uint32_t n_seg = 0, n_samples = 0, n_pixels = 0;
@@ -170,7 +176,7 @@ void render_gwalk_kernel(KParams P) {
         for (int u = 0; u < PRIM_EVERY; u++) {
           if constexpr (COUNT) cn.walk_slots++;
           if (node < end) {
-            walk_box<COUNT, WMEM>(ws, node, r, tmin_c, closest, cn);
+            walk_box<COUNT, WMEM>(ws, node, r, tmin_c, closest, cn, KEEP_SKIP ? &nskip : nullptr);
             if constexpr (COUNT) cn.steps++;
           } else if constexpr (COUNT) {
             if (walk_pending(node)) cn.park_slots++;
@@ -181,7 +187,7 @@ void render_gwalk_kernel(KParams P) {
          * walks on; the wave runs the pending programs once `batch` lanes are blocked or none can step */
         if (walk_pending(node) && pend == G::NONE) {
           pend = node - WALK_PEND;
-          node = walk_successor<WMEM>(ws, pend);
+          node = KEEP_SKIP ? nskip : walk_successor<WMEM>(ws, pend);
         }
         const bool waiting = pend != G::NONE && !(node < end);
         const unsigned long long pm = __ballot(waiting);
@@ -202,7 +208,7 @@ void render_gwalk_kernel(KParams P) {
             pend = G::NONE;
             if (walk_pending(node)) {
               pend = node - WALK_PEND;
-              node = walk_successor<WMEM>(ws, pend);
+              node = KEEP_SKIP ? nskip : walk_successor<WMEM>(ws, pend);
             }
           }
           if constexpr (COUNT) pc.leaf += __builtin_amdgcn_s_memtime() - t_leaf;

@@ -14,6 +14,10 @@ using namespace hrt::kern;
 #define HRT_SPEC 1 /* speculative walk of the walk stream (0: lanes park on every passed leaf, for A/B) */
 #endif
 
+#ifndef HRT_KEEP_SKIP
+#define HRT_KEEP_SKIP 1 /* a parked lane continues at the skip kept from its leaf's step (lane.h walk_box), not at the
+                           successor read from the leaf's payload (0: the payload read, for A/B) */
+#endif
 #ifndef HRT_HEAVY_WAVES
 #define HRT_HEAVY_WAVES 4 /* HEAVY: the out-of-line texture calls spill live registers at 80 VGPRs (6 waves) */
 #endif
@@ -98,6 +102,10 @@ void render_basic_kernel(KParams P) {
   TRay r;
   set_ray(r, ps.ro, ps.rd, 0.0f, P);
   uint32_t node = G::NONE, winner = G::NONE; /* node: walk position (basic_box: index | WALK_PEND, or NONE) */
+  /* hybrid streams only: there the payload read is a global one; from LDS it is cheaper than the register
+   * (C2's kernel: 32 -> 48 B of scratch with it) */
+  constexpr bool KEEP_SKIP = HRT_KEEP_SKIP != 0 && WMEM == WM_HYB;
+  uint32_t nskip = G::NONE; /* KEEP_SKIP: the skip link of the lane's last node step */
   /* SPEC: a passed leaf whose test waits for the wave's next primitive block while the lane walks on
    * (speculative traversal: the walk runs ahead with a closest that the pending test may still shrink,
    * so it visits a superset of the nodes; the leaf tests, each with the reference box test against the
@@ -158,7 +166,8 @@ void render_basic_kernel(KParams P) {
         if (node < end) {
           if constexpr (COUNT) cn.steps++;
           if constexpr (WS) walk_box<COUNT, WMEM, HRT_BOX_FMA && ((WMEM != WM_HYB && !HEAVY) || HRT_BOX_FMA_ALL), false,
-                                    SPLIT ? G::WALK_SPLIT_HALF : 16u, C16>(ws, node, r, tmin_c, closest, cn); /* no rects: no NaN hits (lane.h set_noinv) */
+                                    SPLIT ? G::WALK_SPLIT_HALF : 16u, C16>(ws, node, r, tmin_c, closest, cn,
+                                                                             KEEP_SKIP && SPEC ? &nskip : nullptr); /* no rects: no NaN hits (lane.h set_noinv) */
           else basic_box<CULL, COUNT, STRIDE>(P, nodes, node, r, closest, cn);
         } else if constexpr (COUNT) {
           if (walk_pend<C16>(node)) cn.park_slots++;
@@ -170,7 +179,7 @@ void render_basic_kernel(KParams P) {
            * it; a lane parks for good (blocked) only on a second leaf, or at the end of its walk */
           if (walk_pend<C16>(node) && pend == G::NONE) {
             pend = pend_payload<C16>(P, node);
-            node = walk_successor<WMEM>(ws, pend);
+            node = KEEP_SKIP ? nskip : walk_successor<WMEM>(ws, pend);
           }
           const bool waiting = pend != G::NONE && !(node < end);
           const unsigned long long pm = __ballot(waiting);
@@ -182,7 +191,7 @@ void render_basic_kernel(KParams P) {
               pend = G::NONE;
               if (walk_pend<C16>(node)) { /* blocked: its leaf's test becomes the pending one */
                 pend = pend_payload<C16>(P, node);
-                node = walk_successor<WMEM>(ws, pend);
+                node = KEEP_SKIP ? nskip : walk_successor<WMEM>(ws, pend);
               }
             }
             if constexpr (COUNT) pc.leaf += __builtin_amdgcn_s_memtime() - t_leaf;

@@ -24,6 +24,7 @@ ap.add_argument("--commit-env", default="", help="/-list of NAME=VALUE[,...] env
 ap.add_argument("--count", action="store_true", help="also run one instrumented pass per variant")
 ap.add_argument("--options", default="", help="/-list of NAME=VALUE[,...] hrt_scene_options (chunk_min, chunk_max, "
                 "chunk_uniform, walk_tree, bvh_ties): one scene per setting, alternated (A/B)")
+ap.add_argument("--view", action="store_true", help="commit with hrt_scene_set_view(the camera), as bench.py does")
 ap.add_argument("--share", type=int, default=1, help="render rank 0's share of an N-way tile split (hrt/tiling.py)")
 a = ap.parse_args()
 
@@ -50,6 +51,8 @@ for kind, ce in variants:
     if kind == "env":
         set_env(ce)
     sc = hrt.preset(a.preset, 1, hrt.load_image(_earth) if os.path.exists(_earth) else None, options=opts)
+    if a.view and hasattr(hrt.load(), "hrt_scene_set_view"):  # bench.py's default placement hint
+        sc.set_view(hrt.preset_camera(sc.info, a.width, a.height))
     sc.commit(0)
     if kind == "env":
         clear_env(ce)

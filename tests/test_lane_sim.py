@@ -650,3 +650,27 @@ def test_view_placement_renders_the_same_frame(sim, earth, name, kernel, region)
         assert sb["nodes"] < sa["nodes"], (sa["nodes"], sb["nodes"])
     assert np.array_equal(a, b)
     print(name, "node visits", sa["nodes"], "->", sb["nodes"])
+
+
+@pytest.mark.parametrize("name", ["random", "random_10k", "final", "cornell", "cornell_smoke", "motion", "features"])
+def test_leaf_skip_is_its_payload_successor(earth, name):
+    """layout.h: a leaf's skip link equals the pre-order successor its payload keeps, in every stream (sphere and
+    general, with and without a view).  The hybrid walk kernels continue a parked lane at the skip kept from the
+    leaf's step instead of reading the successor from the payload (lane.h walk_box, HRT_KEEP_SKIP)."""
+    for view in (False, True):
+        s = hrt.preset(name, 1, earth)
+        if view:
+            s.set_view(hrt.preset_camera(s.info, 800, 600))
+        b, i = hrt.scene_blob(s)
+        assert i.walk_bytes > 0 and not i.walk_c16
+        u = np.frombuffer(bytes(b)[i.off_walk:i.off_walk + i.walk_bytes], np.uint32)
+        leaves, stack = 0, [0]
+        while stack:
+            off = stack.pop()
+            skip, pas = int(u[off // 4 + 3]), int(u[off // 4 + 7])
+            if pas & 0x80000000:
+                leaves += 1
+                assert int(u[(pas & 0x7FFFFFFF) // 4 + 3]) >> 2 == skip, (name, off)
+            else:
+                stack += [int(u[pas // 4 + 3]), pas]
+        assert leaves > 0
