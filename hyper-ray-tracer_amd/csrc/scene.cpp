@@ -594,16 +594,19 @@ Aabb box_union(const Aabb& a, const Aabb& b) {
 /* ---- hrt_scene_set_view: what the hierarchy builders use of the view (performance only: any hierarchy over
  * the reference leaf order, placed anywhere, renders the same image, DESIGN.md sections 4-5) */
 /* f64 slab test of b on [lo, hi]; an axis whose product is NaN (0 x inf: the origin on a slab plane) is skipped.
- * On a hit, *entry = the entry t.  For nested boxes the outcome is monotone (a superset passes whenever a
- * subset does: rounding is monotone). */
+ * On a hit, *entry = the t where the ray enters the box, or -inf when its origin lies inside (a leaf box around
+ * the camera, such as Final's fog, stops no ray).  For nested boxes the outcome is monotone (a superset passes
+ * whenever a subset does: rounding is monotone). */
 static bool view_slab(const Aabb& b, const double* o, const double* inv, double lo, double hi, double* entry = nullptr) {
+  double in = -HUGE_VAL;
   for (int k = 0; k < 3; k++) {
     const double t0 = (b.mn[k] - o[k]) * inv[k], t1 = (b.mx[k] - o[k]) * inv[k];
     const double a = std::min(t0, t1), c = std::max(t0, t1);
-    if (a == a) lo = std::max(lo, a);
+    if (a == a) in = std::max(in, a);
     if (c == c) hi = std::min(hi, c);
   }
-  if (entry) *entry = lo;
+  lo = std::max(lo, in);
+  if (entry) *entry = in > 0.0 ? in : -HUGE_VAL;
   return lo <= hi;
 }
 /* a pinhole camera ray through (u, v) of the view's image plane (lens and shutter ignored) */
@@ -631,7 +634,7 @@ static ViewRays view_rays(const hrt_camera& c, const std::vector<WalkLeaf>& leav
     view_ray(c, (q % VIEW_DP_GRID + 0.5) / VIEW_DP_GRID, (q / VIEW_DP_GRID + 0.5) / VIEW_DP_GRID, &R.o[3 * q], &R.inv[3 * q]);
     for (const WalkLeaf& L : leaves) {
       double t;
-      if (view_slab(L.box, &R.o[3 * q], &R.inv[3 * q], VIEW_TMIN, R.cl[q], &t)) R.cl[q] = t;
+      if (view_slab(L.box, &R.o[3 * q], &R.inv[3 * q], VIEW_TMIN, R.cl[q], &t) && t > VIEW_TMIN) R.cl[q] = t;
     }
   }
   return R;
@@ -1085,7 +1088,7 @@ static std::vector<uint32_t> view_heat(const hrt_camera& c, const std::vector<WN
         heat[i]++;
         double t;
         if (view_slab(T[i].box, o, inv, VIEW_TMIN, closest, &t)) {
-          if (T[i].leaf >= 0) closest = std::min(closest, t);
+          if (T[i].leaf >= 0 && t > VIEW_TMIN) closest = std::min(closest, t);
           i++;
         } else {
           i = T[i].end;
@@ -1755,7 +1758,9 @@ void build_walk(hrt_scene* s) {
     if (regroup_ok && s->opts.walk_tree == 0) {
       const auto t0 = std::chrono::steady_clock::now();
       T.clear();
-      walk_regroup(T, leaves, s->has_view ? &s->view : nullptr);
+      /* general streams keep the surface-area DP: with the view's rays Final walks 64.4 -> 65.4 node visits per
+       * segment (lane simulator); the view still places their staged part */
+      walk_regroup(T, leaves, nullptr);
       s->w_build_us = (uint32_t)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
       s->w_regrouped = true;
     }
@@ -1775,7 +1780,7 @@ void build_walk(hrt_scene* s) {
       s->w_general = true;
       if (gok && s->opts.walk_tree == 0) {
         TG.clear();
-        walk_regroup(TG, gl, s->has_view ? &s->view : nullptr);
+        walk_regroup(TG, gl, nullptr); /* general stream: the surface-area DP (above) */
         s->w_regrouped = true;
       }
       walk_place_and_write(s, TG, gl);
