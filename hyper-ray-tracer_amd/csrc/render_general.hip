@@ -30,8 +30,9 @@ namespace {
 
 constexpr int GWALK_WAVES = HRT_GWALK_WAVES;
 #ifndef HRT_GWALK_KEEP_SKIP
-#define HRT_GWALK_KEEP_SKIP 1 /* hybrid streams: a parked lane continues at the skip kept from its leaf's step (lane.h
-                                 walk_box) instead of the successor read from the payload in global memory */
+#define HRT_GWALK_KEEP_SKIP 1 /* a parked lane continues at the skip kept from its leaf's step (lane.h walk_box)
+                                 instead of the successor read from the payload (hybrid streams: a global read,
+                                 Final +2.9%; in LDS: C5's share +1.8%, profiles/r05_keep_skip_ab.txt) */
 #endif
 #ifndef HRT_GWALK_RECOMPUTE
 #define HRT_GWALK_RECOMPUTE 1 /* kernel_common.h claim_work<RECOMPUTE> */
@@ -118,7 +119,7 @@ void render_gwalk_kernel(KParams P) {
   TRay r;
   set_ray(r, ps.ro, ps.rd, 0.0f, P);
   uint32_t node = G::NONE, winner = G::NONE, pend = G::NONE;
-  constexpr bool KEEP_SKIP = HRT_GWALK_KEEP_SKIP != 0 && WMEM == WM_HYB;
+  constexpr bool KEEP_SKIP = HRT_GWALK_KEEP_SKIP != 0;
   uint32_t nskip = G::NONE; /* KEEP_SKIP: the skip link of the lane's last node step */
   uint32_t gstate = G::NONE; /* the last leaf group whose box this walk tested, and its outcome (bit 31) */
   float closest = inf;

@@ -102,9 +102,10 @@ void render_basic_kernel(KParams P) {
   TRay r;
   set_ray(r, ps.ro, ps.rd, 0.0f, P);
   uint32_t node = G::NONE, winner = G::NONE; /* node: walk position (basic_box: index | WALK_PEND, or NONE) */
-  /* hybrid streams only: there the payload read is a global one; from LDS it is cheaper than the register
-   * (C2's kernel: 32 -> 48 B of scratch with it) */
-  constexpr bool KEEP_SKIP = HRT_KEEP_SKIP != 0 && WMEM == WM_HYB;
+  /* every stream: in a hybrid one the payload read is a dependent global read (C4's 1/8 share +2.7%); from LDS it
+   * is a dependent LDS read, and the register is worth more than the 16 B of scratch it adds (C2 +1.8%, C3 +0.7%,
+   * profiles/r05_keep_skip_ab.txt) */
+  constexpr bool KEEP_SKIP = HRT_KEEP_SKIP != 0;
   uint32_t nskip = G::NONE; /* KEEP_SKIP: the skip link of the lane's last node step */
   /* SPEC: a passed leaf whose test waits for the wave's next primitive block while the lane walks on
    * (speculative traversal: the walk runs ahead with a closest that the pending test may still shrink,
