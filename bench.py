@@ -494,8 +494,12 @@ def main():
     dev = torch.device("cuda", local)
     devices = rank_devices(dev, rank, local, world)
     if world > 1 and not args.one_device and distinct_devices(devices) != world:
-        raise SystemExit(f"bench.py: {world} ranks run on {distinct_devices(devices)} distinct devices "
-                         "(--one-device rehearses N ranks on one GPU)")
+        if len({d["device"] for d in devices}) == world:  # distinct HIP devices whose PCI / UUID fields collide
+            log(f"warning: {world} ranks on {world} HIP device indices report {distinct_devices(devices)} distinct "
+                "PCI addresses / UUIDs", all_ranks=True)
+        else:
+            raise SystemExit(f"bench.py: {world} ranks run on {distinct_devices(devices)} distinct devices "
+                             "(--one-device rehearses N ranks on one GPU)")
     turns = args.one_device and world > 1 and args.rehearsal == "turns"
 
     share_of = world if (world > 1 and args.scaling == "tiles") else max(1, args.share)
