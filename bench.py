@@ -100,11 +100,10 @@ def parse():
                          "'auto' = 2 for a short launch of a tile share (stream_count), else 1")
     ap.add_argument("--allow-knobs", action="store_true",
                     help="print the line even when A/B environment knobs of the library are set (never for a headline)")
-    ap.add_argument("--chunks", choices=["auto", "frame"], default="auto",
-                    help="sample-chunk schedule (hrt_scene_options): 'frame' = the library's default for the frame; "
-                         "'auto' = that, or 8-sample chunks when one GPU renders at most a quarter of the frame in a "
-                         "short launch (its end comes sooner: C2's 1/8 share +6%%).  Every rank and the 1-GPU check "
-                         "frame use the same schedule, so the delivered frame stays bit-identical")
+    ap.add_argument("--chunks", default="frame",
+                    help="sample-chunk schedule (hrt_scene_options): 'frame' (default) = the library's schedule for the "
+                         "frame, the same at every GPU count; an integer k = chunks of at least k samples (A/B lines "
+                         "only: the image then differs from the default frame in its low bits)")
     ap.add_argument("--view", choices=["camera", "none"], default="camera",
                     help="hrt_scene_set_view before commit: 'camera' = the rendered camera (a walk stream beyond LDS "
                          "stages the node parts its rays visit most: C4, Final), 'none' = the largest-box ranking.  "
@@ -162,19 +161,19 @@ def distinct_devices(devices):
     return len({(d["pci"], d["uuid"]) for d in devices})
 
 
-SHORT_LAUNCH_SAMPLES = 500e6  # below this many samples per GPU a launch's end is a visible part of it
 OVERLAP_LAUNCH_SAMPLES = 600e6  # stream_count: C2's halves (518 M samples) still gain from overlapping steps
 
 
-def chunk_options(args, share):
-    """hrt_scene_options for the run's sample chunks (--chunks): a GPU rendering at most a quarter of the frame
-    in a short launch (under SHORT_LAUNCH_SAMPLES primary samples: C2's shares; not C4's or C5's, whose 1/8 shares
-    run for a second or more) sums each pixel's samples in chunks of at least 8 (at most 64 of them) instead of
-    the frame default's 16 / 32: the launch's last items are shorter (profiles/r05_share_chunks_ab.txt: C2's 1/8
-    share 12 337 -> 13 104 Mrays/s; the whole frame 14 825 -> 14 647, so one GPU keeps the default)."""
-    if args.chunks == "auto" and share >= 4 and args.width * args.height * args.spp / share < SHORT_LAUNCH_SAMPLES:
-        return {"chunk_min": 8, "chunk_max": 64}
-    return None
+def chunk_options(args):
+    """hrt_scene_options for the run's sample chunks (--chunks).  'frame' (the default, every headline and every
+    N > 1 line): None, the library's schedule, a function of the frame alone (spp, scene class, full image size),
+    so the image is the same bits at every GPU count.  An integer k: chunks of at least k samples
+    (at most 64 of them), an A/B line only; its frame_check then compares with the default frame and reports
+    the difference instead of bit identity.  (r05 switched C2's shares at 4 and 8 GPUs to 8-sample chunks, which
+    made the 4- and 8-GPU images differ in their low bits from the 1-GPU image: VERDICT r05, missing 2.)"""
+    if args.chunks == "frame":
+        return None
+    return {"chunk_min": int(args.chunks), "chunk_max": 64}
 
 
 def stream_count(args, share):
@@ -269,6 +268,42 @@ def cpu_leg(args, frame_rays_per_sample):
                         f"cgroup cpu.max quota {quota if quota else 'none'})",
     }
     return cb, rows, img, c
+
+
+def rows_parity(args, frame, band_render, frame_rays_per_sample):
+    """The metric's own figure on a whole delivered frame (1 GPU, or rank 0's gathered N-GPU frame): the oracle
+    (cpu_leg) on full-width rows spread over the frame at full spp, and the per-pixel L-inf of the frame's rows
+    against it.  `frame` is the (H, W, 4) frame (numpy or a tensor); band_render(rows) renders those rows again
+    on this process's GPU and returns (pixels (len(rows), W, 4), world.hit count), so the GPU's ray count of the
+    rows is compared with the oracle's and the band with the frame's rows (the delivered frame is what was
+    checked).  Returns (cpu_baseline, parity)."""
+    import numpy as np
+
+    cpu, rows, ref_rows, cnt = cpu_leg(args, frame_rays_per_sample)
+    if args.no_parity:
+        return cpu, None
+    got = frame[torch.tensor(rows, device=frame.device)].cpu().numpy() if torch.is_tensor(frame) else np.asarray(frame)[rows]
+    band_px, band_segs = band_render(rows)
+    band_same = bool((np.asarray(band_px) == got).all())
+    linf = float(abs(got - ref_rows).max())
+    rays_equal = int(band_segs) == cnt["segments"]
+    parity = {"linf": linf, "tol": TOL, "pass": bool(linf <= TOL and rays_equal and band_same), "rays_equal": rays_equal,
+              "gpu_rays": int(band_segs), "cpu_rays": cnt["segments"], "rows": len(rows),
+              "pixels": len(rows) * args.width, "spp": args.spp, "band_render_equals_frame_rows": band_same,
+              "reference": "oracle/ CPU restatement of the reference path, same seed and samples"}
+    return cpu, parity
+
+
+def parity_plan(world, rank, share, tiled, args):
+    """Which CPU leg rank 0 runs after the timed steps (the other ranks wait at a barrier, no GPU work):
+    'tiles' for one GPU's share of a split (--share N, the C4 / C5 config lines), 'rows' for a whole frame:
+    one GPU's, the frame gathered from N ranks' tile shares, or rank 0's replica (--scaling weak: sample
+    offset 0, the same frame); None on other ranks or without the CPU leg.  Every N prints both."""
+    if rank != 0 or args.no_cpu_baseline:
+        return None
+    if world == 1 and share > 1:
+        return "tiles"
+    return "rows"
 
 
 def spread_tiles(tiles, n, W, H):
@@ -503,7 +538,7 @@ def main():
     turns = args.one_device and world > 1 and args.rehearsal == "turns"
 
     share_of = world if (world > 1 and args.scaling == "tiles") else max(1, args.share)
-    options = chunk_options(args, share_of)
+    options = chunk_options(args)
     scene = hrt.preset(args.preset, 1, earth_image(), options=options)
     W, H = args.width, args.height
     cam = hrt.preset_camera(scene.info, W, H)
@@ -631,20 +666,37 @@ def main():
                            "gather_ms": None if deliv else round(gather_s * 1e3, 1), "tile": args.tile,
                            "rank_launch_ms": rank_ms, "imbalance": round(max(rank_ms) / max(1e-9, min(rank_ms)), 4)}
             if not args.no_frame_check:
+                # the reference is a 1-GPU render of the whole frame with the DEFAULT options (the headline
+                # frame's schedule): the N-GPU image must be those bits, whatever N
+                ref_scene = scene
+                if options is not None:  # an A/B chunk schedule: the default frame comes from a default scene
+                    ref_scene = hrt.preset(args.preset, 1, earth_image())
+                    if args.view == "camera":
+                        ref_scene.set_view(cam)
+                    ref_scene.commit(local)
                 ref = torch.empty(W * H * 4, dtype=torch.float32, device=dev)
                 p1 = hrt.params(W, H, args.spp, args.depth, args.seed, bg)
-                hrt.render_tiles_device(scene, cam, p1, [(0, 0, W, H)], ref.data_ptr(), stream.cuda_stream)
+                hrt.render_tiles_device(ref_scene, cam, p1, [(0, 0, W, H)], ref.data_ptr(), stream.cuda_stream)
                 torch.cuda.synchronize(dev)
-                same = bool((ref.view(H, W, 4).cpu().numpy() == frame).all())
+                ref_np = ref.view(H, W, 4).cpu().numpy()
+                same = bool((ref_np == frame).all())
                 frame_check["bit_identical_to_1gpu_frame"] = same
-                if not same:
+                frame_check["reference_frame"] = "1-GPU render of the whole frame, default scene options"
+                if options is not None:
+                    frame_check["linf_vs_1gpu_frame"] = float(abs(ref_np - frame).max())
+                    frame_check["chunk_options"] = options
+                elif not same:
                     raise SystemExit("gathered multi-GPU frame differs from the 1-GPU frame")
+                del ref_scene
         barrier()
-    elif world == 1 and share == 1:
+    elif not tiled or share == 1:
+        # one GPU's whole frame, or (weak scaling) rank 0's replica: sample offset 0, the default frame; its
+        # delivery placed every replica over one shared frame, so the check reads rank 0's own output
         frame = out.view(H, W, 4)
 
     cpu, parity = None, None
-    if rank == 0 and world == 1 and share > 1 and not args.no_cpu_baseline:
+    plan = parity_plan(world, rank, share, tiled, args)
+    if plan == "tiles":
         # one GPU's share (C4 / C5 config lines): the oracle on tiles spread over the share, and the metric's
         # L-inf on those tiles of the timed launch's packed output
         cpu, picks, ref_px, cnt = cpu_leg_tiles(args, tiles, seg_step / max(1, samples_step))
@@ -664,20 +716,20 @@ def main():
                       "gpu_rays": int(band.segments), "cpu_rays": cnt["segments"], "tiles": len(picks),
                       "pixels": tiling.share_pixels(sel), "spp": args.spp, "band_render_equals_share_tiles": band_same,
                       "reference": "oracle/ CPU restatement of the reference path, same seed and samples"}
-    elif rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu, rows, ref_rows, cnt = cpu_leg(args, seg_step / max(1, samples_step))
-        if not args.no_parity:
-            got = out.view(H, W, 4)[torch.tensor(rows, device=dev)].cpu().numpy()
+    elif plan == "rows":
+        # the whole frame: 1 GPU's timed frame, or at N > 1 the frame delivered from every rank's share (tiles)
+        # or rank 0's replica (weak, sample offset 0): the rows of THAT frame against the oracle
+        def band_render(rows):
             band_out = torch.empty(len(rows) * W * 4, dtype=torch.float32, device=dev)
-            band = hrt.render_tiles_device(scene, cam, p, [(0, y, W, 1) for y in rows], band_out.data_ptr(),
+            st_b = hrt.render_tiles_device(scene, cam, p, [(0, y, W, 1) for y in rows], band_out.data_ptr(),
                                            stream.cuda_stream, want_stats=True)
-            band_same = bool((band_out.view(len(rows), W, 4).cpu().numpy() == got).all())
-            linf = float(abs(got - ref_rows).max())
-            rays_equal = int(band.segments) == cnt["segments"]
-            parity = {"linf": linf, "tol": TOL, "pass": bool(linf <= TOL and rays_equal), "rays_equal": rays_equal,
-                      "gpu_rays": int(band.segments), "cpu_rays": cnt["segments"], "rows": len(rows),
-                      "pixels": len(rows) * W, "spp": args.spp, "band_render_equals_frame_rows": band_same,
-                      "reference": "oracle/ CPU restatement of the reference path, same seed and samples"}
+            return band_out.view(len(rows), W, 4).cpu().numpy(), int(st_b.segments)
+
+        cpu, parity = rows_parity(args, frame, band_render, seg_all / max(1.0, samples_all))
+        if parity is not None and world > 1:
+            parity["frame"] = ("the frame delivered from the N ranks' tile shares" if tiled
+                               else "rank 0's replica (sample offset 0)")
+    barrier()  # the other ranks wait for rank 0's CPU leg here, with no GPU work
 
     roofline = None
     if rank == 0:
@@ -742,6 +794,7 @@ def main():
                                "the ranks launched at once and their persistent grids contended for the GPU"))
         print(json.dumps(line), flush=True)
     if world > 1:
+        barrier()  # every rank ends with rank 0's line
         torch.distributed.destroy_process_group()
 
 

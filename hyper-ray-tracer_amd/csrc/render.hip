@@ -686,6 +686,23 @@ void launch_name(const char* pretty, char* out, size_t cap) {
 }
 }  // namespace
 
+/* The knobs this launch ran with: those set now (read by the launch) and those set when its scene
+ * was committed (placement knobs, "commit:NAME=value"), snapshotted into the thread's launch record, so a knob
+ * set for the commit and unset before the launch is still reported. */
+void launch_knobs(const hrt_scene* s) {
+  std::string k = knobs_in_effect();
+  size_t a = 0;
+  const std::string& c = s->commit_knobs;
+  while (a < c.size()) {
+    size_t b = c.find(';', a);
+    if (b == std::string::npos) b = c.size();
+    if (!k.empty()) k += ';';
+    k += "commit:" + c.substr(a, b - a);
+    a = b + 1;
+  }
+  snprintf(t_last_launch.knobs, sizeof(t_last_launch.knobs), "%s", k.c_str());
+}
+
 int resident_grid(const void* fn, int block, int device, size_t smem, bool lds, const char* name) {
   static std::mutex mu;
   static std::vector<GridKey> cache;
@@ -933,6 +950,7 @@ hrt_status hrt_render_tiles_device(hrt_scene* s, const hrt_camera* cam, const hr
     kp.partial = (float4*)sl.d_partial;
     if (p->flags & HRT_RENDER_COUNT_WORK) launch_any<true>(s, pl, kp, stream);
     else launch_any<false>(s, pl, kp, stream);
+    launch_knobs(s);
     if (n_chunks > 1) {
       uint32_t blocks = (uint32_t)std::min<uint64_t>((outp + 255) / 256, 4096);
       hipLaunchKernelGGL(reduce_chunks, dim3(blocks), dim3(256), 0, stream, (const float4*)sl.d_partial,
@@ -1181,7 +1199,9 @@ hrt_status hrt_debug_sample_chunks(hrt_scene* s, const hrt_render_params* p, uin
   return hguard([&] {
     if (!s || !p || !out4) throw HipError{HRT_ERR_INVALID_ARG, "hrt_debug_sample_chunks: null argument"};
     if (p->samples == 0) throw HipError{HRT_ERR_INVALID_ARG, "hrt_debug_sample_chunks: no samples"};
-    if (!s->committed) flatten_scene(s);
+    /* the schedule needs the scene's class only (feature mask, main stream length): an uncommitted scene is
+     * flattened without its walk streams (no view pass, no re-grouping) */
+    if (!s->committed) flatten_scene_reference(s);
     chunk_schedule(s, p, out4[0], out4[1], out4[2], out4[3]);
   });
 }
@@ -1190,8 +1210,7 @@ hrt_status hrt_last_launch(hrt_launch_info* out) {
   return hguard([&] {
     if (!out) throw HipError{HRT_ERR_INVALID_ARG, "hrt_last_launch: null pointer"};
     if (!t_has_launch) throw HipError{HRT_ERR_STATE, "hrt_last_launch: no launch on this thread yet"};
-    *out = t_last_launch;
-    snprintf(out->knobs, sizeof(out->knobs), "%s", knobs_in_effect().c_str());
+    *out = t_last_launch; /* knobs: the snapshot taken at that launch (launch_knobs) */
   });
 }
 

@@ -807,7 +807,9 @@ void build_walk(hrt_scene* s);
 namespace {
 using hrt::build_walk;
 
-void flatten(hrt_scene* s) {
+/* The reference node stream, primitives, instances, media, materials, textures and the facts derived from them
+ * (feature mask, culling mode, motion): everything but the walk streams (flatten). */
+void flatten_reference(hrt_scene* s) {
   s->g_nodes.clear(); s->g_prims.clear(); s->g_insts.clear(); s->g_media.clear();
   s->g_mats.clear(); s->g_texs.clear();
   s->feature_mask = 0;
@@ -880,7 +882,6 @@ void flatten(hrt_scene* s) {
   }
   /* Default culling: the reference's per-axis test AND the provably safe inflated slab test
    * (layout.h CULL_EXACT; boxes that may not hold their geometry are flagged NODE_REF_ONLY). */
-  bool sphere_only = (s->feature_mask & (G::F_RECT | G::F_INSTANCE | G::F_MEDIUM)) == 0;
   s->cull_mode = G::CULL_EXACT;
   s->ln_e = ln_f(E_F);
   /* moving_sphere.rs:55-58 divides by (time1 - time0) per call; when every moving sphere has the
@@ -900,6 +901,11 @@ void flatten(hrt_scene* s) {
   if (first) s->motion_uniform = false; /* no moving sphere */
   s->media_nested = false;
   for (const G::Medium& m : s->g_media) s->media_nested |= m.parent != G::NONE;
+}
+
+void flatten(hrt_scene* s) {
+  flatten_reference(s);
+  const bool sphere_only = (s->feature_mask & (G::F_RECT | G::F_INSTANCE | G::F_MEDIUM)) == 0;
   s->f_nodes.clear();
   s->f_prims.clear();
   s->f_stream_len = 0;
@@ -1804,6 +1810,7 @@ void build_walk(hrt_scene* s) {
 }  // namespace hrt
 namespace hrt {
 void flatten_scene(hrt_scene* s) { flatten(s); }
+void flatten_scene_reference(hrt_scene* s) { flatten_reference(s); }
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -1852,7 +1859,8 @@ std::vector<uint8_t> build_blob(hrt_scene* s) {
 extern "C" {
 
 const char* hrt_last_error(void) { return g_error.c_str(); }
-const char* hrt_version(void) { return "hrt 0.1.0 (gfx950)"; }
+const char* hrt_version(void) { return "hrt 0.6.0 (gfx950)"; }
+uint32_t hrt_abi_version(void) { return HRT_ABI_VERSION; }
 
 hrt_status hrt_scene_create(hrt_scene** out) {
   return guard([&] {
@@ -2216,6 +2224,7 @@ hrt_status hrt_scene_commit(hrt_scene* s, int32_t device) {
   hrt_status st = guard([&] {
     mutable_scene(s);
     need(s->root != G::NONE, HRT_ERR_STATE, "no root set");
+    s->commit_knobs = knobs_in_effect(); /* what the walk builders and the upload read */
     flatten(s);
   });
   if (st != HRT_OK) return st;

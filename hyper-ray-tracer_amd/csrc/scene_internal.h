@@ -104,6 +104,7 @@ struct hrt_scene {
   uint32_t bvh_tied_sorts = 0; /* BvhNode::new sorts of > 20 objects with equal keys (hrt_scene_info) */
   uint32_t n_media = 0;
   bool committed = false;
+  std::string commit_knobs; /* knobs_in_effect() when hrt_scene_commit ran (placement knobs act there) */
   hrt_scene_options opts{}; /* explicit configuration (hrt_scene_set_options); all-zero = default */
   bool has_view = false;    /* placement hint (hrt_scene_set_view): the camera most renders will use */
   hrt_camera view{};
@@ -179,6 +180,8 @@ void set_error(const std::string& msg);
 /* implemented in render.hip */
 hrt_status device_upload(hrt_scene* s, int device);
 void flatten_scene(hrt_scene* s);          /* scene.cpp: graph -> layout.h arrays */
+void flatten_scene_reference(hrt_scene* s); /* ... without the walk streams (the reference stream and the facts
+                                               derived from it: feature mask, main_end) */
 std::vector<uint8_t> build_blob(hrt_scene* s); /* scene.cpp: the arrays in one blob; sets s->off_* */
 /* scene.cpp: the walk stream's leaves (with the reference hierarchy and whether it may be re-grouped),
  * and the placement + records of a hierarchy over them */

@@ -149,13 +149,13 @@ class SceneOptions(ctypes.Structure):
 
 
 # Diagnostics an older build may lack; only tolerated when HRT_LIB points at another build (A/B runs)
-OPTIONAL = {"hrt_last_launch", "hrt_debug_box_test", "hrt_scene_set_options", "hrt_scene_get_options",
+OPTIONAL = {"hrt_abi_version", "hrt_last_launch", "hrt_debug_box_test", "hrt_scene_set_options", "hrt_scene_get_options",
             "hrt_debug_sample_chunks", "hrt_scene_set_view"}
 HRT_LIB_OVERRIDE = bool(os.environ.get("HRT_LIB"))
 
 # Every entry point of include/hrt/hrt.h (tests/test_abi.py checks the header against this list).
 EXPORTS = [
-    "hrt_last_error", "hrt_version", "hrt_scene_create", "hrt_scene_destroy",
+    "hrt_last_error", "hrt_version", "hrt_abi_version", "hrt_scene_create", "hrt_scene_destroy",
     "hrt_tex_solid", "hrt_tex_checker", "hrt_tex_noise", "hrt_tex_image",
     "hrt_mat_lambertian", "hrt_mat_metal", "hrt_mat_dielectric", "hrt_mat_diffuse_light", "hrt_mat_isotropic",
     "hrt_node_sphere", "hrt_node_moving_sphere", "hrt_node_rect", "hrt_node_cuboid", "hrt_node_translate",
@@ -167,6 +167,7 @@ EXPORTS = [
     "hrt_debug_sample_chunks", "hrt_scene_set_view",
 ]
 
+ABI_VERSION = 6  # include/hrt/hrt.h HRT_ABI_VERSION: the struct layouts below
 _lib = None
 _U32P = ctypes.POINTER(ctypes.c_uint32)
 _F3 = ctypes.c_float * 3
@@ -194,6 +195,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     sig = {
         "hrt_last_error": (ctypes.c_char_p, []),
         "hrt_version": (ctypes.c_char_p, []),
+        "hrt_abi_version": (ctypes.c_uint32, []),
         "hrt_scene_create": (S, [ctypes.POINTER(vp)]),
         "hrt_scene_destroy": (None, [vp]),
         "hrt_tex_solid": (S, [vp, f, f, f, _U32P]),
@@ -248,6 +250,9 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
+    if hasattr(L, "hrt_abi_version") and L.hrt_abi_version() != ABI_VERSION and not HRT_LIB_OVERRIDE:
+        raise RuntimeError(f"{path}: ABI version {L.hrt_abi_version()}, this binding is written for {ABI_VERSION} "
+                           "(include/hrt/hrt.h HRT_ABI_VERSION): rebuild the library")
     _lib = L
     return L
 

@@ -32,11 +32,31 @@ ENV_KEYS = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR
 SPAWNED = "HRT_BENCH_SPAWNED"  # set in the children: the line records who launched the ranks
 
 
+class ProfilerPreloadError(RuntimeError):
+    """This process runs under a profiler's preloaded library and would have to start its ranks."""
+
+
+def profiler_preloaded(env: Optional[Dict[str, str]] = None) -> bool:
+    """True when a profiler's library (rocprofv3's tool library, rocprof's) is in LD_PRELOAD: it may initialise
+    the GPU before main runs, so this process must not start other programs."""
+    env = os.environ if env is None else env
+    pre = env.get("LD_PRELOAD", "")
+    return any(k in os.path.basename(x) for x in pre.replace(":", " ").split() for k in ("rocprof", "roctracer"))
+
+
 def needs_spawn(gpus: int, env: Optional[Dict[str, str]] = None) -> bool:
     """True when this process must start its own ranks: more than one GPU asked for and no launcher
-    (torch.distributed.run, or this module) has set up a process group environment."""
+    (torch.distributed.run, or this module) has set up a process group environment.  Raises
+    ProfilerPreloadError when that process runs under a profiler's preload: profile each rank as its own
+    program instead (set RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR, MASTER_PORT and put
+    `rocprofv3 ... --` in front of each; scripts/gpu.sh rehtrace does)."""
     env = os.environ if env is None else env
-    return gpus > 1 and "WORLD_SIZE" not in env and "RANK" not in env
+    spawn = gpus > 1 and "WORLD_SIZE" not in env and "RANK" not in env
+    if spawn and profiler_preloaded(env):
+        raise ProfilerPreloadError(
+            "bench.py --gpus N under a profiler would start its ranks from a process the profiler's preload may "
+            "have attached to the GPU: run one profiled process per rank with the process-group variables set")
+    return spawn
 
 
 def free_port(addr: str = "127.0.0.1") -> int:

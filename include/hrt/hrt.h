@@ -160,6 +160,14 @@ enum {
 
 const char* hrt_last_error(void);
 const char* hrt_version(void);
+/* ABI version.  Structs the library writes (hrt_render_stats, hrt_launch_info, hrt_blob_info) have
+ * grown between releases with no size field, so a caller built against an older header would be written past
+ * its buffers: check hrt_abi_version() == HRT_ABI_VERSION once before any other call, and rebuild on a mismatch.
+ *   6: hrt_abi_version; hrt_launch_info.knobs is the launch's snapshot, commit-time knobs as "commit:NAME=value"
+ *   5: hrt_launch_info.knobs (+256 B), hrt_render_stats.walk_steps, hrt_blob_info walk_c16/walk_nodes/walk_pbase,
+ *      hrt_scene_options, hrt_scene_set_view, hrt_debug_sample_chunks */
+#define HRT_ABI_VERSION 6u
+uint32_t hrt_abi_version(void);
 
 /* ---- scene lifetime ---- */
 hrt_status hrt_scene_create(hrt_scene** out);
@@ -368,7 +376,8 @@ typedef struct hrt_blob_info {
   uint32_t walk_pbase;     /* walk_c16: byte offset of the payloads */
 } hrt_blob_info;
 hrt_status hrt_debug_scene_blob(hrt_scene* s, void* out, uint64_t cap, uint64_t* size, hrt_blob_info* info);
-/* The sample chunks a render of these params would use (no device involved; flattens an uncommitted scene):
+/* The sample chunks a render of these params would use (no device involved; an uncommitted scene is flattened
+ * without its walk streams, which the schedule does not depend on):
  * out[0] = chunk size, out[1] = head chunks, out[2] = samples of the first chunk, out[3] = halving tail chunks.
  * A pixel's samples are summed chunk by chunk and the chunk sums added in chunk order, so this schedule is
  * what fixes the image's bits beyond the paths themselves (hrt_scene_options chunk_*). */

@@ -83,13 +83,21 @@ step() {
       echo "== $tag: 2-rank rehearsal $*" >> "$LOG"
       timeout -k 10 240 python -u bench.py --gpus 2 --one-device "$@" >> "$OUT/$tag.jsonl" 2>> "$OUT/$tag.err"
       local rc=$?; echo "== $tag exit $rc" >> "$LOG"; return $rc ;;
-    rehtrace)  # kernel timeline of a concurrent 2-rank rehearsal (both ranks' launches on one GPU clock)
+    rehtrace)  # kernel timeline of a concurrent 2-rank rehearsal: one rocprofv3 per rank (each rank its own
+      # profiled program with the process-group variables set, so bench.py never spawns under the profiler's preload)
       local tag=$1; shift
       echo "== $tag: rocprofv3 kernel trace of a 2-rank rehearsal $*" >> "$LOG"
       export TMPDIR=/tmp
-      timeout -k 10 300 rocprofv3 --kernel-trace -d "$OUT/prof_${tag}" -o run_%pid% --output-format csv -- \
-        python3 "$ROOT/bench.py" --gpus 2 --one-device "$@" >> "$OUT/$tag.jsonl" 2>> "$OUT/$tag.err"
-      local rc=$?; echo "== $tag exit $rc" >> "$LOG"; return $rc ;;
+      local port=$(( 29500 + RANDOM % 2000 )) pids=() r rc=0
+      for r in 0 1; do
+        RANK=$r LOCAL_RANK=$r WORLD_SIZE=2 LOCAL_WORLD_SIZE=2 MASTER_ADDR=127.0.0.1 MASTER_PORT=$port \
+          timeout -k 10 300 rocprofv3 --kernel-trace -d "$OUT/prof_${tag}/rank$r" -o run --output-format csv -- \
+          python3 "$ROOT/bench.py" --gpus 2 --one-device "$@" >> "$OUT/$tag.r$r.out" 2>> "$OUT/$tag.err" &
+        pids+=($!)
+      done
+      for r in 0 1; do wait "${pids[$r]}" || rc=$?; done
+      cat "$OUT/$tag.r0.out" >> "$OUT/$tag.jsonl"
+      echo "== $tag exit $rc" >> "$LOG"; return $rc ;;
     configs)
       local tag=$1
       # C3 with its parity rows and CPU baseline; C4's whole frame with the fewest rows the CPU budget allows (a 4K

@@ -44,19 +44,29 @@ def test_pmc_key_names_the_share_and_rejects_counters_above_peak():
     assert ro["frac"] is None and ro["pmc_key"] == "k"
 
 
-def test_chunk_schedule_per_run():
-    """--chunks auto: 8-sample chunks only for a GPU rendering at most a quarter of the frame in a short launch
-    (C2's shares at 4 and 8 GPUs); one GPU, C2's halves and C4's / C5's long share launches keep the frame's."""
-    def args(w, h, spp, chunks="auto"):
-        return argparse.Namespace(width=w, height=h, spp=spp, chunks=chunks)
-    short = {"chunk_min": 8, "chunk_max": 64}
-    assert bench.chunk_options(args(1920, 1080, 500), 1) is None
-    assert bench.chunk_options(args(1920, 1080, 500), 2) is None
-    assert bench.chunk_options(args(1920, 1080, 500), 4) == short
-    assert bench.chunk_options(args(1920, 1080, 500), 8) == short
-    assert bench.chunk_options(args(1920, 1080, 500, "frame"), 8) is None
-    assert bench.chunk_options(args(3840, 2160, 2000), 8) is None   # C4: 2.07 G samples per GPU
-    assert bench.chunk_options(args(2048, 2048, 10000), 8) is None  # C5
+def test_chunk_schedule_is_the_frames_at_every_gpu_count():
+    """VERDICT r05 (missing 2): the sample chunks are a function of the frame alone, so the image is the same bits
+    at 1, 2, 4 and 8 GPUs.  No share or GPU count enters chunk_options; only an explicit A/B value changes it."""
+    import inspect
+
+    def args(chunks="frame"):
+        return argparse.Namespace(width=1920, height=1080, spp=500, chunks=chunks)
+    assert bench.chunk_options(args()) is None
+    assert list(inspect.signature(bench.chunk_options).parameters) == ["args"]
+    assert bench.chunk_options(args("8")) == {"chunk_min": 8, "chunk_max": 64}
+
+
+def test_every_gpu_count_gets_parity_and_cpu_baseline():
+    """VERDICT r05 (missing 1): rank 0 runs the CPU leg at every N (the oracle rows of the delivered N-GPU frame,
+    or of its replica under weak scaling); a one-GPU share line uses tiles; other ranks run none."""
+    a = argparse.Namespace(no_cpu_baseline=False)
+    for world in (1, 2, 4, 8):
+        assert bench.parity_plan(world, 0, world, True, a) == "rows"
+        assert bench.parity_plan(world, 0, 1, False, a) == "rows"
+        for r in range(1, world):
+            assert bench.parity_plan(world, r, world, True, a) is None
+    assert bench.parity_plan(1, 0, 8, True, a) == "tiles"
+    assert bench.parity_plan(2, 0, 2, True, argparse.Namespace(no_cpu_baseline=True)) is None
 
 
 def test_share_tiles_for_the_cpu_leg_spread_in_two_dimensions():

@@ -172,6 +172,47 @@ def test_tiling_split_on_gpu(world, earth):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_bench_split_equals_default_1gpu_frame(world, earth):
+    """VERDICT r05 (missing 2): the image is the same bits at every GPU count.  Every rank's scene is built as
+    bench.py builds it at N = `world` (its chunk options, the rendered camera as the view hint), its share
+    rendered as bench.py's timed steps do (two alternating streams for C2's short shares), placed, and the frame
+    compared with a DEFAULT 1-GPU render (no options, no view) of C2's scene at its full 500 spp."""
+    import argparse
+
+    import torch
+
+    import bench
+    from hrt import tiling
+
+    W, H, spp = 320, 180, 500
+    a = argparse.Namespace(width=1920, height=1080, spp=spp, chunks="frame", streams="auto")
+    ref_scene = hrt.preset("random", 1, earth)
+    ref_scene.commit()
+    cam = hrt.preset_camera(ref_scene.info, W, H)
+    p = hrt.params(W, H, spp, 50, 1, tuple(ref_scene.info.background))
+    full = hrt.render(ref_scene, cam, p)
+    s = hrt.preset("random", 1, earth, options=bench.chunk_options(a))
+    s.set_view(cam)
+    s.commit()
+    n_str = bench.stream_count(a, world)
+    streams = [torch.cuda.Stream() for _ in range(n_str)]
+    frame = np.full((H, W, 4), np.nan, np.float32)
+    outs = []
+    for r in range(world):
+        t = tiling.split_tiles(W, H, world, r)
+        d = torch.empty(tiling.share_pixels(t) * 4, dtype=torch.float32, device="cuda")
+        hrt.render_tiles_device(s, cam, p, t, d.data_ptr(), streams[r % n_str].cuda_stream)
+        outs.append((t, d))
+    torch.cuda.synchronize()
+    s.synchronize()
+    for t, d in outs:
+        tiling.place_tiles(frame, t, d.cpu().numpy())
+    assert hrt.sample_chunks(s, p) == hrt.sample_chunks(ref_scene, p)
+    assert np.array_equal(frame, full)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name,W,H,spp", [("random", 400, 225, 50), ("final", 200, 200, 16), ("random_10k", 320, 180, 8)])
 def test_bvh_tie_order_sensitivity(name, W, H, spp, earth, monkeypatch):
     """BvhNode::new sorts with Rust's sort_unstable_by (bvh_node.rs:34); for more than 20 objects with equal

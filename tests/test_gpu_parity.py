@@ -442,7 +442,26 @@ def test_final_walk_variants_are_bit_identical(earth, monkeypatch, knob):
     s2.commit()
     b, sb = hrt.render(s2, cam, p, stats=True)
     assert sa.segments == sb.segments and np.array_equal(a, b), knob
-    assert hrt.last_launch()["knobs"] == knob, hrt.last_launch()["knobs"]  # the launch reports the A/B knob
+    # the launch reports the A/B knob, as read at the launch and at the scene's commit
+    assert hrt.last_launch()["knobs"].split(";") == [knob, "commit:" + knob], hrt.last_launch()["knobs"]
+
+
+@pytest.mark.gpu
+def test_commit_knob_is_reported_after_it_is_unset(earth, monkeypatch):
+    """a placement knob set while the scene is committed and unset before the launch still shows in
+    the launch's record (hrt_launch_info.knobs, "commit:NAME=value"), so bench.py refuses such a line."""
+    w, h, spp = 48, 32, 4
+    monkeypatch.setenv("HRT_GWALK_BIG", "0")
+    s = hrt.preset("final", 1, earth)
+    s.commit()
+    monkeypatch.delenv("HRT_GWALK_BIG")
+    cam = hrt.preset_camera(s.info, w, h)
+    hrt.render(s, cam, hrt.params(w, h, spp, 50, 5, tuple(s.info.background)))
+    assert hrt.last_launch()["knobs"] == "commit:HRT_GWALK_BIG=0"
+    s2 = hrt.preset("final", 1, earth)
+    s2.commit()
+    hrt.render(s2, cam, hrt.params(w, h, spp, 50, 5, tuple(s2.info.background)))
+    assert hrt.last_launch()["knobs"] == ""
 
 
 @pytest.mark.gpu

@@ -22,6 +22,19 @@ def test_needs_spawn_only_without_a_launcher():
     assert not launcher.needs_spawn(2, {"RANK": "1"})
 
 
+def test_no_spawn_under_a_profiler_preload():
+    """a process under rocprofv3's preloaded library must not start the ranks itself; profiled ranks
+    run as their own programs with the process-group variables set (scripts/gpu.sh rehtrace)."""
+    import pytest
+
+    pre = {"LD_PRELOAD": "/opt/rocm/lib/rocprofiler-sdk/librocprofiler-sdk-tool.so"}
+    with pytest.raises(launcher.ProfilerPreloadError):
+        launcher.needs_spawn(2, pre)
+    assert not launcher.needs_spawn(1, pre)
+    assert not launcher.needs_spawn(2, {**pre, "WORLD_SIZE": "2", "RANK": "0"})
+    assert launcher.needs_spawn(2, {"LD_PRELOAD": "/usr/lib/libfoo.so"})
+
+
 def test_child_env_is_torchrun_shaped():
     base = {"PATH": "/bin", "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
     e = launcher.child_env(base, 3, 8, 29555)

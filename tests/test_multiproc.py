@@ -189,3 +189,50 @@ def test_delivery_error_path_ends_every_rank():
         pass
     assert err is not None and "failed" in err
     assert dt < 30
+
+
+def _parity_worker(rank, world, port, q):
+    """bench.py at N > 1: every rank renders its tile share (the oracle standing in for its GPU), the shares are
+    gathered to rank 0, and rank 0 runs bench.rows_parity on the gathered frame while the others wait."""
+    import argparse
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "hyper-ray-tracer_amd"), root]
+    import hrt
+    from hrt import tiling
+    from oracle import oracle as O
+    import bench
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    o = O.OracleScene(hrt.PRESETS["random"], 1)
+    packed, _ = _render_share(o, tiling.split_tiles(W, H, world, rank))
+    frame = tiling.gather_frame(packed, W, H, world, rank)
+    if rank == 0:
+        args = argparse.Namespace(preset="random", width=W, height=H, spp=SPP, depth=DEPTH, seed=SEED, cpu_seconds=0.2,
+                                  no_parity=False, no_cpu_baseline=False)
+        assert bench.parity_plan(world, rank, world, True, args) == "rows"
+
+        def band_render(rows):  # the GPU's band render, the oracle standing in
+            img, cnt = o.render_rows(W, H, SPP, rows, DEPTH, seed=SEED, threads=2)
+            return img, cnt["segments"]
+
+        cpu, parity = bench.rows_parity(args, frame, band_render, 2.8)
+        q.put((cpu, parity))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_multi_rank_line_has_parity_and_cpu_baseline():
+    """an N > 1 line carries the metric's own L-inf (rows of the frame gathered from the ranks'
+    shares against the oracle, equal ray counts) and the CPU baseline, as the 1-GPU line does."""
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    pc = mp.start_processes(_parity_worker, args=(2, _free_port(), q), nprocs=2, join=False, start_method="spawn")
+    cpu, parity = q.get()
+    while not pc.join(timeout=60):
+        pass
+    assert parity["pass"] and parity["rays_equal"] and parity["band_render_equals_frame_rows"]
+    assert parity["linf"] == 0.0 and parity["rows"] >= 2
+    assert cpu["value"] > 0 and cpu["kind"] == "port" and cpu["cores"] >= 1
