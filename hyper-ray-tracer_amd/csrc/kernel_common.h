@@ -30,8 +30,8 @@ void launch_sphere(int cull, bool count, bool lds, bool heavy, const lane::KPara
                    size_t smem);
 /* render_general.hip: launch render_gwalk_kernel (wmem: lane.h WM_*, lref: reference stream in LDS,
  * trim: lane.h TRIM_* features compiled out) */
-void launch_gwalk(bool count, int wmem, bool lref, int trim, bool one, const lane::KParams& kp, int device, hipStream_t stream,
-                  size_t smem);
+void launch_gwalk(bool count, int wmem, bool lref, int trim, bool one, bool packet, const lane::KParams& kp, int device,
+                  hipStream_t stream, size_t smem);
 
 namespace kern {
 namespace G = hrt::gpu;

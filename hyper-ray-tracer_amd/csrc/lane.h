@@ -940,7 +940,7 @@ HRT_LANE Rec make_record(const KParams& P, uint32_t winner, float t, Vec3 wo, Ve
 /* perlin_noise.rs:80-123 over tables read through `pn`: a generic pointer, or (device, tables staged in LDS by
  * the kernel) an LDS address-space pointer, so the 8 x 4 gathers per call are ds_read, not flat loads */
 #ifndef HRT_PERLIN_SELECT
-#define HRT_PERLIN_SELECT 0
+#define HRT_PERLIN_SELECT 1 /* r06: C3 +1.3% (17 218 -> 17 445 Mrays/s, profiles/r06_perlin_select_ab.txt) */
 #endif
 template <class PN>
 HRT_LANE_FI float perlin_noise_t(PN pn, Vec3 point) {
@@ -954,7 +954,7 @@ HRT_LANE_FI float perlin_noise_t(PN pn, Vec3 point) {
   v = v * v * (3.0f - 2.0f * v);
   w = w * w * (3.0f - 2.0f * w);
 #if HRT_PERLIN_SELECT
-  /* opt-in (unmeasured on the GPU): perlin_noise.rs:108-114's factor x u + (1 - x)(1 - u) for x in {0, 1} is
+  /* default since r06 (0: the reference's multiply form): perlin_noise.rs:108-114's factor x u + (1 - x)(1 - u) for x in {0, 1} is
    * exactly (1 - u) or u -- u is in [0, 1] or NaN, so 0 u = +0, the sum adds +0 to a value >= 0 (or NaN to
    * NaN) and 1 v = v -- without the multiplies and adds strict IEEE code keeps (12 VALU per octave;
    * tests/test_lane_sim.py checks both forms against the oracle bit for bit) */

@@ -210,6 +210,9 @@ static_assert(2u * (LDS_SCENE_MAX_BYTES + 768u * 4u) <= 160u * 1024u, "two spher
  * BIG) with the node parts a ray is likeliest to reach in LDS, twice the two-workgroup budget */
 constexpr uint32_t GWALK_LDS_BIG_BYTES = 152u * 1024u;
 static_assert(GWALK_LDS_BIG_BYTES + 1024u * 4u <= 160u * 1024u, "one 1024-thread general workgroup per CU");
+/* general streams of at most this many node parts (staged whole in LDS with their reference arrays) are walked
+ * by each wave as one packet (render_general.hip PACKET): Cornell 35, Cornell-smoke, simple-light */
+constexpr uint32_t GWALK_PACKET_NODES = 128u;
 constexpr uint32_t WALK_NODE_BYTES = 32, WALK_PAYLOAD_BYTES = 96;
 /* Split node parts (r04, sphere streams staged whole in LDS): a node part's first 16 B (C, skip) at its
  * offset, its second 16 B (E, pass) WALK_SPLIT_HALF bytes further (an immediate offset of the LDS read),

@@ -375,6 +375,7 @@ struct Plan {
   bool gwalk;    /* general scene on render_gwalk_kernel (the general walk stream, render_general.hip) */
   int gwalk_mem; /* its walk-stream placement: WM_LDS / WM_HYB / WM_BUF */
   bool gwalk_lref; /* ... with the reference stream and primitives staged in LDS too */
+  bool gwalk_packet; /* ... walked by the wave as one packet (a small stream staged whole in LDS) */
   int gen_waves; /* general scenes under CULL_EXACT: the render_kernel<FULL> instantiation (3 or 4 waves/SIMD) */
   int trim;      /* general scenes: features compiled out of render_kernel (lane.h TRIM_*) */
   bool general; /* sphere scene forced onto the general kernel (diagnostics: HRT_KERNEL=general) */
@@ -445,6 +446,7 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
              !(k && (strcmp(k, "general") == 0 || strcmp(k, "persistent") == 0 || strcmp(k, "segment") == 0));
   pl.gwalk_mem = WM_BUF;
   pl.gwalk_lref = false;
+  pl.gwalk_packet = false;
   if (pl.gwalk) {
     pl.general = false;
     const size_t walk = s->w_hot ? s->w_hot : s->w_end;
@@ -465,11 +467,18 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
     pl.perlin_lds = pl.gwalk_lref && perlin > 0 && pl.smem + perlin <= LDS_SCENE_MAX && !(pe && strcmp(pe, "0") == 0);
     if (pl.perlin_lds) pl.smem += perlin;
     pl.lds = pl.gwalk_mem != WM_BUF;
+    /* the packet walk (render_general.hip) for streams of at most GWALK_PACKET_NODES node parts staged whole in
+     * LDS with their reference arrays whose leaves run generic programs (s->w_generic: Cornell-smoke's media in
+     * rotated boxes): a wave's lanes visit at most that many nodes together per segment */
+    const char* pk = knob_env("HRT_GWALK_PACKET"); /* A/B knob: "0" keeps the per-lane speculative walk, "1" forces it */
+    pl.gwalk_packet = pl.gwalk_lref && s->w_nodes <= G::GWALK_PACKET_NODES &&
+                      (pk ? strcmp(pk, "1") == 0 : s->w_generic);
     pl.trim = ((s->feature_mask & (G::F_NOISE | G::F_IMAGE)) == 0 ? TRIM_HEAVY_TEX : 0) |
               ((s->feature_mask & G::F_MEDIUM) == 0 ? TRIM_MEDIA : 0);
     const char* tp = knob_env("HRT_GWALK_TRIMP"); /* A/B knob: "0" keeps trace_ray's generic program compiled in */
     if (!s->w_generic && !(tp && strcmp(tp, "0") == 0)) pl.trim |= TRIM_PROGRAMS;
     if (lt && strcmp(lt, "0") == 0) pl.trim = 0;
+    if (pl.trim & TRIM_PROGRAMS) pl.gwalk_packet = false; /* instantiated with the generic program only */
   }
   return pl;
 }
@@ -481,7 +490,7 @@ void launch_any(const hrt_scene* s, const Plan& pl, const KParams& kp, hipStream
     /* every chunk one sample (head of 1-sample chunks, no tail): render_gwalk_kernel's ONE instantiation */
     const char* o1 = knob_env("HRT_GWALK_ONE"); /* A/B knob: "0" keeps the general chunk loop */
     const bool one = kp.chunk == 1u && kp.chunk_first == 1u && kp.n_chunks == kp.chunk_head && !(o1 && strcmp(o1, "0") == 0);
-    launch_gwalk(COUNT, pl.gwalk_mem, pl.gwalk_lref, pl.trim, one, kp, s->device, stream, smem);
+    launch_gwalk(COUNT, pl.gwalk_mem, pl.gwalk_lref, pl.trim, one, pl.gwalk_packet, kp, s->device, stream, smem);
     return;
   }
   if (pl.fast) {

@@ -46,7 +46,9 @@ constexpr int GWALK_WAVES = HRT_GWALK_WAVES;
  * a lane's work item is dead once its sample has started and its partial sum is that sample's radiance, so
  * neither the item nor the chunk's running sum lives across the walk and shading (Final: 48 -> 32 B of
  * scratch per lane; the spills that were left were per-segment writes, 3.9 GB per launch). */
-template <bool COUNT, int WMEM, bool LREF, int TRIM, bool BIG, bool ONE>
+/* PACKET: the wave walks a small stream staged whole in LDS, whose leaves run generic programs (Cornell-smoke's
+ * media in rotated boxes), as one packet: see below */
+template <bool COUNT, int WMEM, bool LREF, int TRIM, bool BIG, bool ONE, bool PACKET>
 __global__ __launch_bounds__((BIG ? 256 : 128) * GWALK_WAVES, GWALK_WAVES)
 void render_gwalk_kernel(KParams P) {
   extern __shared__ float4 lds_scene[];
@@ -169,6 +171,54 @@ void render_gwalk_kernel(KParams P) {
     const unsigned long long walkers = __ballot(walking);
     uint32_t iters = 0;
     bool stuck = false;
+    if constexpr (PACKET) {
+      /* The packet walk (small streams staged whole in LDS with generic leaf programs).  The wave keeps ONE walk
+       * position u (wave-uniform) and every lane its own: a lane is active at u when its position is u.  At an
+       * inner node the active lanes run the inflated test and move to `pass` or `skip`; the wave goes to `pass`
+       * if any lane passed, else to `skip`.  At a leaf the passing lanes run the leaf's program at once, all of
+       * them together (one leaf, one kind: the program's code is uniform), and every active lane moves to the
+       * leaf's skip.  In pre-order a lane's own position is always u or beyond u's subtree, so every lane
+       * visits exactly the nodes of its own stackless walk, in the same order and with the same closest (the
+       * non-speculative walk: each leaf tested as it is reached), and all lanes end their segment together:
+       * no parked lanes, no postponed shading, one uniform node read (an LDS broadcast) per step.  The price: the
+       * wave visits the union of its lanes' nodes.  Measured (profiles/r06_packet_ab.txt): Cornell-smoke +14%
+       * (its leaf programs, two media in rotated boxes, run once for all the lanes that need them instead of
+       * parking lanes in batches); Cornell -42% and simple-light -11% (one-node programs: the per-lane walk's
+       * batches cost less than visiting the union), so those keep the per-lane walk. */
+      if (__ballot(node < end)) {
+        uint32_t u = 0u;
+        while (u < end) {
+          if constexpr (COUNT) cn.walk_slots++;
+          const float4 a = wload<WM_LDS>(ws, u), b = wload<WM_LDS>(ws, u + 16u);
+          const uint32_t skip = (uint32_t)__builtin_amdgcn_readfirstlane((int)f2u(a.w));
+          const uint32_t pass = (uint32_t)__builtin_amdgcn_readfirstlane((int)f2u(b.w));
+          const bool act = node == u;
+          bool p = false;
+          if (act) {
+            if constexpr (COUNT) {
+              cn.nodes++;
+              cn.steps++;
+            }
+            p = box_ce<HRT_BOX_FMA != 0, true>(a, b, r, tmin_c, closest);
+          }
+          uint32_t nu;
+          if (walk_pending(pass)) { /* a leaf (uniform): its program for the lanes that passed, now */
+            if (p) gwalk_leaf_test<MEDIA, COUNT, WMEM, PROG>(Q, nodes, prims, ws, pass - WALK_PEND, r, closest, winner, gstate,
+                                                             ps.pk, cn);
+            if (act) node = skip;
+            nu = skip;
+          } else {
+            if (act) node = p ? pass : skip;
+            nu = __ballot(p) ? pass : skip;
+          }
+          if (nu <= u) { /* links point forward in a valid stream: a corrupt one is reported, not walked */
+            stuck = true;
+            break;
+          }
+          u = nu;
+        }
+      }
+    } else {
     for (;;) {
       /* the node steps unrolled on their own, the leaf block after every PRIM_EVERY of them: unrolling
        * the block with them made the loop too large for the unroller */
@@ -218,6 +268,7 @@ void render_gwalk_kernel(KParams P) {
       const unsigned long long live = __ballot(node < end || walk_pending(node) || pend != G::NONE);
       if (!live || (uint32_t)__popcll(walkers & ~live) >= need) break;
       if (++iters > cap) { stuck = true; break; }
+    }
     }
     if (stuck) {
       if (lane == 0) atomicOr(&P.stats[12], 1ull);
@@ -292,20 +343,22 @@ void render_gwalk_kernel(KParams P) {
   }
 }
 
-template <bool COUNT, int WMEM, bool LREF, int TRIM, bool BIG = false, bool ONE = false>
+template <bool COUNT, int WMEM, bool LREF, int TRIM, bool BIG = false, bool ONE = false, bool PACKET = false>
 void launch_g(const KParams& kp, int device, hipStream_t stream, size_t smem) {
-  const void* fn = (const void*)render_gwalk_kernel<COUNT, WMEM, LREF, TRIM, BIG, ONE>;
+  const void* fn = (const void*)render_gwalk_kernel<COUNT, WMEM, LREF, TRIM, BIG, ONE, PACKET>;
   const int block = (BIG ? 256 : 128) * GWALK_WAVES;
   KParams p = kp;
   p.lane_lds = (uint32_t)((smem + 15) & ~(size_t)15);
   const size_t total = p.lane_lds + (size_t)block * sizeof(uint32_t);
   const int grid = resident_grid(fn, block, device, total, true, __PRETTY_FUNCTION__);
-  hipLaunchKernelGGL((render_gwalk_kernel<COUNT, WMEM, LREF, TRIM, BIG, ONE>), dim3(grid), dim3(block), total, stream, p);
+  hipLaunchKernelGGL((render_gwalk_kernel<COUNT, WMEM, LREF, TRIM, BIG, ONE, PACKET>), dim3(grid), dim3(block), total, stream, p);
   hip_check(hipGetLastError(), "render_gwalk_kernel launch");
 }
 
 template <bool COUNT, int TRIM>
-void launch_g_mem(int wmem, bool lref, bool one, const KParams& kp, int device, hipStream_t stream, size_t smem) {
+void launch_g_mem(int wmem, bool lref, bool one, bool packet, const KParams& kp, int device, hipStream_t stream, size_t smem) {
+  if constexpr (!(TRIM & TRIM_PROGRAMS)) /* packet walks: streams with generic leaf programs (render.hip plan) */
+    if (wmem == WM_LDS && lref && packet) return launch_g<COUNT, WM_LDS, true, TRIM, false, false, true>(kp, device, stream, smem);
   if (wmem == WM_LDS) lref ? launch_g<COUNT, WM_LDS, true, TRIM>(kp, device, stream, smem)
                            : launch_g<COUNT, WM_LDS, false, TRIM>(kp, device, stream, smem);
   else if (wmem == WM_HYB && smem > G::LDS_SCENE_MAX_BYTES) {
@@ -320,27 +373,27 @@ void launch_g_mem(int wmem, bool lref, bool one, const KParams& kp, int device, 
 
 namespace hrt {
 
-void launch_gwalk(bool count, int wmem, bool lref, int trim, bool one, const KParams& kp, int device, hipStream_t stream,
-                  size_t smem) {
+void launch_gwalk(bool count, int wmem, bool lref, int trim, bool one, bool packet, const KParams& kp, int device,
+                  hipStream_t stream, size_t smem) {
   /* instantiated trims: none, media, heavy textures, both; TRIM_PROGRAMS with none (Final) or both (Cornell) */
   if (trim & TRIM_PROGRAMS) {
     const int base = trim & ~TRIM_PROGRAMS;
     if (base != 0 && base != (TRIM_MEDIA | TRIM_HEAVY_TEX)) trim = base;
   }
   if (count) {
-    if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX | TRIM_PROGRAMS)) launch_g_mem<true, TRIM_MEDIA | TRIM_HEAVY_TEX | TRIM_PROGRAMS>(wmem, lref, one, kp, device, stream, smem);
-    else if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX)) launch_g_mem<true, TRIM_MEDIA | TRIM_HEAVY_TEX>(wmem, lref, one, kp, device, stream, smem);
-    else if (trim == TRIM_MEDIA) launch_g_mem<true, TRIM_MEDIA>(wmem, lref, one, kp, device, stream, smem);
-    else if (trim == TRIM_HEAVY_TEX) launch_g_mem<true, TRIM_HEAVY_TEX>(wmem, lref, one, kp, device, stream, smem);
-    else if (trim == TRIM_PROGRAMS) launch_g_mem<true, TRIM_PROGRAMS>(wmem, lref, one, kp, device, stream, smem);
-    else launch_g_mem<true, 0>(wmem, lref, one, kp, device, stream, smem);
+    if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX | TRIM_PROGRAMS)) launch_g_mem<true, TRIM_MEDIA | TRIM_HEAVY_TEX | TRIM_PROGRAMS>(wmem, lref, one, packet, kp, device, stream, smem);
+    else if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX)) launch_g_mem<true, TRIM_MEDIA | TRIM_HEAVY_TEX>(wmem, lref, one, packet, kp, device, stream, smem);
+    else if (trim == TRIM_MEDIA) launch_g_mem<true, TRIM_MEDIA>(wmem, lref, one, packet, kp, device, stream, smem);
+    else if (trim == TRIM_HEAVY_TEX) launch_g_mem<true, TRIM_HEAVY_TEX>(wmem, lref, one, packet, kp, device, stream, smem);
+    else if (trim == TRIM_PROGRAMS) launch_g_mem<true, TRIM_PROGRAMS>(wmem, lref, one, packet, kp, device, stream, smem);
+    else launch_g_mem<true, 0>(wmem, lref, one, packet, kp, device, stream, smem);
   } else {
-    if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX | TRIM_PROGRAMS)) launch_g_mem<false, TRIM_MEDIA | TRIM_HEAVY_TEX | TRIM_PROGRAMS>(wmem, lref, one, kp, device, stream, smem);
-    else if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX)) launch_g_mem<false, TRIM_MEDIA | TRIM_HEAVY_TEX>(wmem, lref, one, kp, device, stream, smem);
-    else if (trim == TRIM_MEDIA) launch_g_mem<false, TRIM_MEDIA>(wmem, lref, one, kp, device, stream, smem);
-    else if (trim == TRIM_HEAVY_TEX) launch_g_mem<false, TRIM_HEAVY_TEX>(wmem, lref, one, kp, device, stream, smem);
-    else if (trim == TRIM_PROGRAMS) launch_g_mem<false, TRIM_PROGRAMS>(wmem, lref, one, kp, device, stream, smem);
-    else launch_g_mem<false, 0>(wmem, lref, one, kp, device, stream, smem);
+    if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX | TRIM_PROGRAMS)) launch_g_mem<false, TRIM_MEDIA | TRIM_HEAVY_TEX | TRIM_PROGRAMS>(wmem, lref, one, packet, kp, device, stream, smem);
+    else if (trim == (TRIM_MEDIA | TRIM_HEAVY_TEX)) launch_g_mem<false, TRIM_MEDIA | TRIM_HEAVY_TEX>(wmem, lref, one, packet, kp, device, stream, smem);
+    else if (trim == TRIM_MEDIA) launch_g_mem<false, TRIM_MEDIA>(wmem, lref, one, packet, kp, device, stream, smem);
+    else if (trim == TRIM_HEAVY_TEX) launch_g_mem<false, TRIM_HEAVY_TEX>(wmem, lref, one, packet, kp, device, stream, smem);
+    else if (trim == TRIM_PROGRAMS) launch_g_mem<false, TRIM_PROGRAMS>(wmem, lref, one, packet, kp, device, stream, smem);
+    else launch_g_mem<false, 0>(wmem, lref, one, packet, kp, device, stream, smem);
   }
 }
 

@@ -220,7 +220,15 @@ def test_general_kernels_are_bit_identical(earth, monkeypatch, name, w, h, spp):
     a, sa = hrt.render(s, cam, p, stats=True)
     pc = hrt.params(w, h, spp, 50, 7, tuple(s.info.background), flags=hrt.RENDER_COUNT_WORK)
     c, sc = hrt.render(s, cam, pc, stats=True)
-    assert sc.prim_slots > 0 and np.array_equal(a, c)
+    packet = "PACKET = true" in hrt.last_launch()["kernel"]
+    assert packet or name != "cornell_smoke", hrt.last_launch()["kernel"]
+    assert (sc.prim_slots > 0 or packet) and np.array_equal(a, c)
+    if packet:  # the per-lane walk of the same kernel (A/B knob): the same frame
+        monkeypatch.setenv("HRT_GWALK_PACKET", "0")
+        d, sd = hrt.render(s, cam, p, stats=True)
+        assert "PACKET = false" in hrt.last_launch()["kernel"]
+        assert sd.segments == sa.segments and np.array_equal(a, d)
+        monkeypatch.delenv("HRT_GWALK_PACKET")
     for kernel in ("segment", "persistent"):
         monkeypatch.setenv("HRT_KERNEL", kernel)
         b, sb = hrt.render(s, cam, p, stats=True)

@@ -475,11 +475,12 @@ def test_final_general_walk_variants(sim, earth, knob, monkeypatch):
 
 @pytest.fixture(scope="module")
 def sim_perlin_select(tmp_path_factory):
-    """The lanes with the opt-in Perlin corner-weight selects (lane.h HRT_PERLIN_SELECT)."""
-    return _build_sim(tmp_path_factory, ("-DHRT_PERLIN_SELECT=1",))
+    """The lanes with the reference's multiply form of the Perlin corner weights (lane.h HRT_PERLIN_SELECT=0; the
+    kernels' default since r06 selects u or 1 - u)."""
+    return _build_sim(tmp_path_factory, ("-DHRT_PERLIN_SELECT=0",))
 
 
-@pytest.mark.parametrize("variant", ["default", "select"])
+@pytest.mark.parametrize("variant", ["default", "multiply"])
 def test_perlin_lane_code_equals_oracle_bit_for_bit(sim, sim_perlin_select, variant):
     """lane.h perlin_noise_t / noise_value_t (the kernels' Perlin) against the oracle's perlin_noise.rs
     restatement on the scene's tables: noise and the noise texture's turbulence term, bit for bit, over points
