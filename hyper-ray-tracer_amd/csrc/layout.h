@@ -222,6 +222,10 @@ constexpr uint32_t WALK_NODE_BYTES = 32, WALK_PAYLOAD_BYTES = 96;
  * no faster on C2 (14 024 vs 14 038 Mrays/s, profiles/r04g_ab.txt), so the conflicts are not what
  * bounds the step. */
 constexpr uint32_t WALK_SPLIT_HALF = 16384;
+/* ... and for hybrid sphere streams (r06, opt-in HRT_WALK_SPLIT=1): pages of 2 x 8 KiB, 512 node parts each,
+ * first halves then second halves (scene.cpp walk_place_and_write); the staged part ends on a page's second
+ * halves, so at most 15 KiB of the 77 KiB budget is left unused */
+constexpr uint32_t WALK_SPLIT_HALF_HYB = 8192;
 /* 16-B node parts (r05, WALK_C16; hybrid sphere streams, the C4 class; opt-in HRT_WALK_C16=1: measured 8% slower
  * on C4's 1/8 share, the binary16 widening and link decode cost more than twice the staged node parts save):
  * the staged budget holds twice the node parts.  A part is four u32: (C.x | C.y << 16), (C.z | E.x << 16), (E.y | E.z << 16), (skip | pass << 16), C and

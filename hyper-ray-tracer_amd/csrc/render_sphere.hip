@@ -29,7 +29,7 @@ constexpr int sphere_waves() { return HEAVY ? HRT_HEAVY_WAVES : BASIC_WAVES; }
 
 /* HYB (CULL_EXACT with LDS): the walk stream exceeds the LDS budget; its first P.walk_hot bytes (the
  * hierarchy's top levels) are staged, the rest is read through the buffer descriptor (layout.h) */
-/* SPLIT: the stream's node parts are split (layout.h WALK_SPLIT_HALF; LDS, not HYB) */
+/* SPLIT: the stream's node parts are split (layout.h WALK_SPLIT_HALF; hybrid streams: WALK_SPLIT_HALF_HYB) */
 /* C16: 16-B node parts (layout.h WALK_C16; hybrid streams): walk positions are node indices */
 template <int CULL, bool COUNT, bool LDS, bool HYB = false, bool HEAVY = false, bool SPLIT = false, bool C16 = false>
 __global__ __launch_bounds__((basic_block_threads<LDS, sphere_waves<HEAVY>()>()), sphere_waves<HEAVY>())
@@ -167,7 +167,7 @@ void render_basic_kernel(KParams P) {
         if (node < end) {
           if constexpr (COUNT) cn.steps++;
           if constexpr (WS) walk_box<COUNT, WMEM, HRT_BOX_FMA && ((WMEM != WM_HYB && !HEAVY) || HRT_BOX_FMA_ALL), false,
-                                    SPLIT ? G::WALK_SPLIT_HALF : 16u, C16>(ws, node, r, tmin_c, closest, cn,
+                                    SPLIT ? (HYB ? G::WALK_SPLIT_HALF_HYB : G::WALK_SPLIT_HALF) : 16u, C16>(ws, node, r, tmin_c, closest, cn,
                                                                              KEEP_SKIP && SPEC ? &nskip : nullptr); /* no rects: no NaN hits (lane.h set_noinv) */
           else basic_box<CULL, COUNT, STRIDE>(P, nodes, node, r, closest, cn);
         } else if constexpr (COUNT) {
@@ -311,7 +311,10 @@ void launch_sphere(int cull, bool count, bool lds, bool heavy, const KParams& kp
     else count ? launch_basic<G::CULL_EXACT, true, false, false, false, false, true>(kp, device, stream, 0)
                : launch_basic<G::CULL_EXACT, false, false, false, false, false, true>(kp, device, stream, 0);
   } else if (cull == G::CULL_EXACT && lds && kp.walk_hot > 0) { /* top levels in LDS, the rest in global memory */
-    if (count) launch_basic<G::CULL_EXACT, true, true, true>(kp, device, stream, smem);
+    if (kp.walk_half != 16u) { /* split node parts (layout.h WALK_SPLIT_HALF_HYB, opt-in) */
+      if (count) launch_basic<G::CULL_EXACT, true, true, true, false, true>(kp, device, stream, smem);
+      else launch_basic<G::CULL_EXACT, false, true, true, false, true>(kp, device, stream, smem);
+    } else if (count) launch_basic<G::CULL_EXACT, true, true, true>(kp, device, stream, smem);
     else launch_basic<G::CULL_EXACT, false, true, true>(kp, device, stream, smem);
   } else if (cull == G::CULL_EXACT && kp.walk_half != 16u) { /* split node parts (layout.h; F_BASIC scenes) */
     if (count) lds ? launch_basic<G::CULL_EXACT, true, true, false, false, true>(kp, device, stream, smem)

@@ -1136,8 +1136,9 @@ static bool walk_place_and_write_impl(hrt_scene* s, const std::vector<WNode>& T,
    * after them (HRT_WALK_PAYLOADS=inline: each payload behind its leaf) */
   const char* hotsel = knob_env("HRT_WALK_HOTSEL");
   const bool by_area = !(hotsel && strcmp(hotsel, "depth") == 0);
+  std::vector<uint32_t> order; /* hybrid: the node parts in staging priority */
   if (hybrid) {
-    std::vector<uint32_t> order(N);
+    order.resize(N);
     for (uint32_t i = 0; i < N; i++) order[i] = i;
     if (s->has_view && by_area) {
       /* hrt_scene_set_view: the node parts the view's camera rays visit most (lane-simulated C4 segments, held-out
@@ -1226,6 +1227,43 @@ static bool walk_place_and_write_impl(hrt_scene* s, const std::vector<WNode>& T,
     }
     END = std::max(q, H2 + 16u * N);
     s->w_half = H2;
+  }
+  /* split node parts of a HYBRID sphere stream (opt-in HRT_WALK_SPLIT=1): pages of 2 x
+   * WALK_SPLIT_HALF_HYB bytes, each holding the first halves of WALK_SPLIT_HALF_HYB / 16 node parts back to back
+   * and their second halves WALK_SPLIT_HALF_HYB further, so the LDS and the buffer reads both find a part's second
+   * half at a fixed immediate offset.  The staged set keeps the hot order, as many parts as fit the budget (a
+   * partial last page staged up to its last second half); the other parts start on the next page, in pre-order;
+   * every payload after the last page. */
+  if (hybrid && !c16 && !s->w_general && (s->feature_mask & ~G::F_BASIC) == 0 && sp_env && strcmp(sp_env, "1") == 0 &&
+      apart) {
+    const uint32_t HH = G::WALK_SPLIT_HALF_HYB, PPP = HH / 16u;
+    auto extent = [&](uint32_t n) { return (n / PPP) * 2u * HH + (n % PPP ? HH + 16u * (n % PPP) : 0u); };
+    auto slot = [&](uint32_t k) { return (k / PPP) * 2u * HH + (k % PPP) * 16u; };
+    uint32_t n_hot = 0;
+    while (n_hot < N && extent(n_hot + 1) <= budget) n_hot++;
+    std::fill(hot.begin(), hot.end(), 0);
+    uint32_t k = 0;
+    for (; k < n_hot; k++) {
+      hot[order[k]] = 1;
+      addr[order[k]] = slot(k);
+    }
+    if (k % PPP) k += PPP - k % PPP; /* the global parts start on a page of their own */
+    for (uint32_t i = 0; i < N; i++)
+      if (!hot[i]) addr[i] = slot(k++);
+    uint32_t q = k % PPP ? (k / PPP) * 2u * HH + HH + 16u * (k % PPP) : (k / PPP) * 2u * HH;
+    for (uint32_t i = 0; i < N; i++) /* payloads: the global leaves' in pre-order, then the staged leaves' */
+      if (T[i].leaf >= 0 && !hot[i]) {
+        paddr[i] = q;
+        q += PB;
+      }
+    for (uint32_t i = 0; i < N; i++)
+      if (T[i].leaf >= 0 && hot[i]) {
+        paddr[i] = q;
+        q += PB;
+      }
+    END = q;
+    s->w_hot = extent(n_hot);
+    s->w_half = HH;
   }
   if (s->w_hot)
     for (uint32_t i = 0; i < N; i++)

@@ -430,6 +430,29 @@ def test_split_node_parts_render_the_same_frame(earth, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_hybrid_split_node_parts_render_the_same_frame(earth, monkeypatch):
+    """layout.h WALK_SPLIT_HALF_HYB (opt-in HRT_WALK_SPLIT=1): the hybrid sphere walk (random-10k) over node parts in
+    8-KB-split pages, LDS and buffer reads alike, renders the default 32-B layout's frame and rays bit for bit."""
+    def render():
+        import torch
+
+        s = hrt.preset("random_10k", 1, earth)
+        cam = hrt.preset_camera(s.info, 384, 216)
+        s.set_view(cam)
+        s.commit()
+        p = hrt.params(384, 216, 16, 50, 3, tuple(s.info.background))
+        d = torch.empty(384 * 216 * 4, dtype=torch.float32, device="cuda")
+        st = hrt.render_tiles_device(s, cam, p, [(0, 0, 384, 216)], d.data_ptr(), 0, want_stats=True)
+        return d.cpu().numpy(), st, hrt.scene_blob(s)[1], hrt.last_launch()["kernel"]
+    a, sa, ia, ka = render()
+    monkeypatch.setenv("HRT_WALK_SPLIT", "1")
+    b, sb, ib, kb = render()
+    assert ia.walk_half == 16 and ib.walk_half == 8192 and ib.walk_hot > 0
+    assert "HYB = true" in kb and "SPLIT = true" in kb, kb
+    assert sa.segments == sb.segments and np.array_equal(a, b)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("knob", ["HRT_GWALK_MED=0", "HRT_GWALK_BIG=0", "HRT_GWALK_TRIMP=0"])
 def test_final_walk_variants_are_bit_identical(earth, monkeypatch, knob):
     """Final through the general walk kernel's r04 variants against the default (flat one-sphere media

@@ -460,6 +460,44 @@ def test_split_node_parts_equal_interleaved(sim, earth, name, monkeypatch):
     assert np.array_equal(a, b)
 
 
+def test_hybrid_split_node_parts_equal_interleaved(sim, earth, monkeypatch):
+    """layout.h WALK_SPLIT_HALF_HYB (r06): a hybrid sphere stream (random-10k: 1.6 MB, its
+    view-ranked node parts staged) in pages of 512 node parts, first halves then second halves 8 KB later, the
+    staged part ending on a page's second halves; the walk over it equals the 32-B layout's bit for bit, and the
+    layout's invariants hold (staged set inside the LDS budget, every payload beyond it, every leaf's skip = the
+    successor its payload keeps)."""
+    s0 = hrt.preset("random_10k", 1, earth)
+    s0.set_view(hrt.preset_camera(s0.info, 96, 54))
+    _, info0 = hrt.scene_blob(s0)
+    monkeypatch.setenv("HRT_WALK_SPLIT", "1")
+    s1 = hrt.preset("random_10k", 1, earth)
+    s1.set_view(hrt.preset_camera(s1.info, 96, 54))
+    blob, info = hrt.scene_blob(s1)
+    assert info.walk_half == 8192 and 0 < info.walk_hot <= 77 * 1024 and info.walk_hot > 70 * 1024
+    assert info.walk_nodes == info0.walk_nodes and info0.walk_half == 16
+    w = np.frombuffer(blob.raw, np.uint8)[info.off_walk:info.off_walk + info.walk_bytes]
+    u = w.view(np.uint32)
+    off, leaves, seen = 0, 0, set()
+    while off < info.walk_bytes:  # pre-order through pass / skip links: every node part once, payloads beyond the staged part
+        assert off not in seen and off % 16 == 0 and (off // 8192) % 2 == 0  # a first half, on a page's first half
+        seen.add(off)
+        skip, pas = int(u[off // 4 + 3]), int(u[(off + 8192) // 4 + 3])
+        if pas & (1 << 31):
+            q = pas - (1 << 31)
+            assert q >= info.walk_hot and int(u[q // 4 + 3]) >> 2 == skip
+            leaves += 1
+            off = skip
+        else:
+            off = pas
+    assert len(seen) == info.walk_nodes and leaves == (info.walk_nodes + 1) // 2
+    monkeypatch.delenv("HRT_WALK_SPLIT")
+    a, sa = sim_render(sim, "random_10k", 48, 27, 4, 50, 5, earth, kernel=0, cull=CULL_EXACT, view=True)
+    monkeypatch.setenv("HRT_WALK_SPLIT", "1")
+    b, sb = sim_render(sim, "random_10k", 48, 27, 4, 50, 5, earth, kernel=0, cull=CULL_EXACT, view=True)
+    assert sa == sb
+    assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("knob", ["HRT_GWALK_MED=0", "HRT_GWALK_BIG=0"])
 def test_final_general_walk_variants(sim, earth, knob, monkeypatch):
     """Final's general walk with a one-sphere medium as a flat program (layout.h GL_MED) and with the 152-KB
