@@ -26,8 +26,8 @@ void hip_check(hipError_t e, const char* what);
  * (`name`: the launcher's __PRETTY_FUNCTION__, whose template arguments name the instantiation) */
 int resident_grid(const void* fn, int block, int device, size_t smem, bool lds, const char* name);
 /* render_sphere.hip: launch render_basic_kernel<cull, count, lds> */
-void launch_sphere(int cull, bool count, bool lds, bool heavy, const lane::KParams& kp, int device, hipStream_t stream,
-                   size_t smem);
+void launch_sphere(int cull, bool count, bool lds, bool heavy, bool packet, const lane::KParams& kp, int device,
+                   hipStream_t stream, size_t smem);
 /* render_general.hip: launch render_gwalk_kernel (wmem: lane.h WM_*, lref: reference stream in LDS,
  * trim: lane.h TRIM_* features compiled out) */
 void launch_gwalk(bool count, int wmem, bool lref, int trim, bool one, bool packet, const lane::KParams& kp, int device,

@@ -25,7 +25,7 @@ static const char* const KNOWN_KNOBS[] = {
     "HRT_CLAIM_FINE",    "HRT_GEN_LDS",      "HRT_GEN_TRIM",       "HRT_GEN_WAVES_RT", "HRT_GWALK",
     "HRT_GWALK_BIG",     "HRT_GWALK_FLAT",   "HRT_GWALK_FLATLIST", "HRT_GWALK_GROUPED", "HRT_GWALK_LREF",
     "HRT_GWALK_MED", "HRT_GWALK_ONE",     "HRT_GWALK_TRIMP",  "HRT_GWALK_PACKET",  "HRT_KERNEL",         "HRT_PERLIN_LDS",   "HRT_POSTPONE",
-    "HRT_PRIM_BATCH",    "HRT_TILE_STRIDE",  "HRT_WALK_BUILD",     "HRT_WALK_DP",      "HRT_WALK_DP_SUB",
+    "HRT_PRIM_BATCH",    "HRT_SPHERE_PACKET",    "HRT_TILE_STRIDE",  "HRT_WALK_BUILD",     "HRT_WALK_DP",      "HRT_WALK_DP_SUB",
     "HRT_WALK_HOT",      "HRT_WALK_HOTSEL",  "HRT_WALK_PAYLOADS",  "HRT_WALK_SPLIT",   "HRT_WALK_C16"};
 
 /* the knobs set in the environment now (a knob acts when read: at commit for placement knobs, at each launch

@@ -322,23 +322,23 @@ HRT_LANE_FI void wload_node(const WalkSrc& src, uint32_t off, float4& a, float4&
     const bool in_lds = off < src.hot;
     const uint32_t loff = in_lds ? off : 0u;
     [[maybe_unused]] const uint32_t goff = in_lds ? 0x7FFFFF00u : off;
-    const float4 la = wload<WM_LDS>(src, loff), lb = wload<WM_LDS>(src, loff + 16u);
+    const float4 la = wload<WM_LDS>(src, loff), lb = wload<WM_LDS>(src, loff + HALF);
 #if HRT_HYB_ANYG == 2
     /* the buffer loads only for the lanes that need them (exec mask), into registers of their own */
     float4 ga = make_float4(0.0f, 0.0f, 0.0f, 0.0f), gb = ga;
     if (!in_lds) {
       ga = wload<WM_BUF>(src, off);
-      gb = wload<WM_BUF>(src, off + 16u);
+      gb = wload<WM_BUF>(src, off + HALF);
     }
 #elif HRT_HYB_ANYG
     /* the buffer loads only when a lane of the wave needs them (a wave-uniform branch) */
     float4 ga = make_float4(0.0f, 0.0f, 0.0f, 0.0f), gb = ga;
     if (__builtin_amdgcn_ballot_w64(!in_lds)) {
       ga = wload<WM_BUF>(src, goff);
-      gb = wload<WM_BUF>(src, goff + 16u);
+      gb = wload<WM_BUF>(src, goff + HALF);
     }
 #else
-    const float4 ga = wload<WM_BUF>(src, goff), gb = wload<WM_BUF>(src, goff + 16u);
+    const float4 ga = wload<WM_BUF>(src, goff), gb = wload<WM_BUF>(src, goff + HALF);
 #endif
     a = in_lds ? la : ga;
     b = in_lds ? lb : gb;

@@ -213,6 +213,9 @@ static_assert(GWALK_LDS_BIG_BYTES + 1024u * 4u <= 160u * 1024u, "one 1024-thread
 /* general streams of at most this many node parts (staged whole in LDS with their reference arrays) are walked
  * by each wave as one packet (render_general.hip PACKET): Cornell 35, Cornell-smoke, simple-light */
 constexpr uint32_t GWALK_PACKET_NODES = 128u;
+/* sphere streams of at most this many node parts (staged whole in LDS) are walked by each wave as one packet
+ * (render_sphere.hip PACKET): Earth + Perlin (C3), Earth, the two-sphere scenes: 3 node parts each */
+constexpr uint32_t SPHERE_PACKET_NODES = 15u;
 constexpr uint32_t WALK_NODE_BYTES = 32, WALK_PAYLOAD_BYTES = 96;
 /* Split node parts (r04, sphere streams staged whole in LDS): a node part's first 16 B (C, skip) at its
  * offset, its second 16 B (E, pass) WALK_SPLIT_HALF bytes further (an immediate offset of the LDS read),

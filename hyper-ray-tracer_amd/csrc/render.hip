@@ -376,6 +376,7 @@ struct Plan {
   int gwalk_mem; /* its walk-stream placement: WM_LDS / WM_HYB / WM_BUF */
   bool gwalk_lref; /* ... with the reference stream and primitives staged in LDS too */
   bool gwalk_packet; /* ... walked by the wave as one packet (a small stream staged whole in LDS) */
+  bool sphere_packet; /* sphere kernel: a tiny walk stream staged whole in LDS walked as one packet */
   int gen_waves; /* general scenes under CULL_EXACT: the render_kernel<FULL> instantiation (3 or 4 waves/SIMD) */
   int trim;      /* general scenes: features compiled out of render_kernel (lane.h TRIM_*) */
   bool general; /* sphere scene forced onto the general kernel (diagnostics: HRT_KERNEL=general) */
@@ -435,6 +436,12 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
     const char* pe = knob_env("HRT_PERLIN_LDS"); /* A/B knob: "0" keeps the Perlin tables in global memory */
     pl.perlin_lds = pl.lds && perlin > 0 && pl.smem + perlin <= LDS_SCENE_MAX && !(pe && strcmp(pe, "0") == 0);
     if (pl.perlin_lds) pl.smem += perlin;
+  }
+  /* the sphere kernel's packet walk (render_sphere.hip PACKET) for streams of at most SPHERE_PACKET_NODES node parts */
+  {
+    const char* sp = knob_env("HRT_SPHERE_PACKET"); /* A/B knob: "0" keeps the per-lane walk, "1" forces the packet */
+    pl.sphere_packet = !pl.full && !pl.fast && pl.lds && pl.cull == G::CULL_EXACT && !s->w_hot && !s->w_general &&
+                       (sp ? strcmp(sp, "1") == 0 : s->w_nodes <= G::SPHERE_PACKET_NODES);
   }
   pl.trim = 0;
   if ((s->feature_mask & (G::F_NOISE | G::F_IMAGE)) == 0)
@@ -526,15 +533,15 @@ void launch_any(const hrt_scene* s, const Plan& pl, const KParams& kp, hipStream
   } else if (pl.cull == G::CULL_EXACT) {
     if (pl.full) pl.lds ? launch_full<G::CULL_EXACT, COUNT, true>(kp, s->device, stream, smem)
                         : launch_full<G::CULL_EXACT, COUNT, false>(kp, s->device, stream, 0);
-    else launch_sphere(G::CULL_EXACT, COUNT, pl.lds, pl.heavy, kp, s->device, stream, smem);
+    else launch_sphere(G::CULL_EXACT, COUNT, pl.lds, pl.heavy, pl.sphere_packet, kp, s->device, stream, smem);
   } else if (pl.cull == G::CULL_SLAB) {
     if (pl.full) pl.lds ? launch_full<G::CULL_SLAB, COUNT, true>(kp, s->device, stream, smem)
                         : launch_full<G::CULL_SLAB, COUNT, false>(kp, s->device, stream, 0);
-    else launch_sphere(G::CULL_SLAB, COUNT, pl.lds, false, kp, s->device, stream, smem);
+    else launch_sphere(G::CULL_SLAB, COUNT, pl.lds, false, false, kp, s->device, stream, smem);
   } else {
     if (pl.full) pl.lds ? launch_full<G::CULL_REFERENCE, COUNT, true>(kp, s->device, stream, smem)
                         : launch_full<G::CULL_REFERENCE, COUNT, false>(kp, s->device, stream, 0);
-    else launch_sphere(G::CULL_REFERENCE, COUNT, pl.lds, false, kp, s->device, stream, smem);
+    else launch_sphere(G::CULL_REFERENCE, COUNT, pl.lds, false, false, kp, s->device, stream, smem);
   }
 }
 

@@ -31,7 +31,10 @@ constexpr int sphere_waves() { return HEAVY ? HRT_HEAVY_WAVES : BASIC_WAVES; }
  * hierarchy's top levels) are staged, the rest is read through the buffer descriptor (layout.h) */
 /* SPLIT: the stream's node parts are split (layout.h WALK_SPLIT_HALF; hybrid streams: WALK_SPLIT_HALF_HYB) */
 /* C16: 16-B node parts (layout.h WALK_C16; hybrid streams): walk positions are node indices */
-template <int CULL, bool COUNT, bool LDS, bool HYB = false, bool HEAVY = false, bool SPLIT = false, bool C16 = false>
+/* PACKET: a tiny stream staged whole in LDS (at most SPHERE_PACKET_NODES node parts: Earth + Perlin, the two-sphere
+ * scenes) walked by the wave as one packet (render_general.hip PACKET): every lane's segment ends in one pass */
+template <int CULL, bool COUNT, bool LDS, bool HYB = false, bool HEAVY = false, bool SPLIT = false, bool C16 = false,
+          bool PACKET = false>
 __global__ __launch_bounds__((basic_block_threads<LDS, sphere_waves<HEAVY>()>()), sphere_waves<HEAVY>())
 void render_basic_kernel(KParams P) {
   extern __shared__ float4 lds_scene[];
@@ -160,6 +163,43 @@ void render_basic_kernel(KParams P) {
     const unsigned long long walkers = __ballot(walking);
     uint32_t iters = 0;
     bool stuck = false;
+    if constexpr (PACKET) {
+      /* the packet walk (render_general.hip PACKET): the wave at ONE position u, the lanes whose own position is u
+       * active; a leaf's test runs at once for the lanes that pass its box, so each lane tests exactly its own
+       * walk's leaves, in order, with its own closest, and every lane's walk ends in this pass */
+      if (__ballot(node < end)) {
+        uint32_t u = 0u;
+        while (u < end) {
+          if constexpr (COUNT) cn.walk_slots++;
+          const float4 a = wload<WM_LDS>(ws, u), b = wload<WM_LDS>(ws, u + 16u);
+          const uint32_t skip = (uint32_t)__builtin_amdgcn_readfirstlane((int)f2u(a.w));
+          const uint32_t pass = (uint32_t)__builtin_amdgcn_readfirstlane((int)f2u(b.w));
+          const bool act = node == u;
+          bool p = false;
+          if (act) {
+            if constexpr (COUNT) {
+              cn.nodes++;
+              cn.steps++;
+            }
+            p = box_ce<HRT_BOX_FMA && !HEAVY, false>(a, b, r, tmin_c, closest);
+          }
+          uint32_t nu;
+          if (walk_pend<false>(pass)) { /* a leaf (uniform) */
+            if (p) walk_leaf_test<COUNT, WMEM>(P, ws, pass - WALK_PEND, r, closest, winner, cn);
+            if (act) node = skip;
+            nu = skip;
+          } else {
+            if (act) node = p ? pass : skip;
+            nu = __ballot(p) ? pass : skip;
+          }
+          if (nu <= u) { /* links point forward in a stream staged whole: a corrupt one is reported */
+            stuck = true;
+            break;
+          }
+          u = nu;
+        }
+      }
+    } else {
     for (;;) {
 #pragma unroll
       for (int u = 0; u < WALK_UNROLL; u++) {
@@ -212,6 +252,7 @@ void render_basic_kernel(KParams P) {
       const unsigned long long live = __ballot(node < end || walk_pend<C16>(node) || (SPEC && pend != G::NONE));
       if (!live || (uint32_t)__popcll(walkers & ~live) >= need) break;
       if (++iters > cap) { stuck = true; break; }
+    }
     }
     if (stuck) { /* a walk that cannot end (corrupt scene data): report it, retire the wave */
       if (lane == 0) atomicOr(&P.stats[12], 1ull);
@@ -272,9 +313,10 @@ void render_basic_kernel(KParams P) {
 }
 
 
-template <int CULL, bool COUNT, bool LDS, bool HYB = false, bool HEAVY = false, bool SPLIT = false, bool C16 = false>
+template <int CULL, bool COUNT, bool LDS, bool HYB = false, bool HEAVY = false, bool SPLIT = false, bool C16 = false,
+          bool PACKET = false>
 void launch_basic(const KParams& kp, int device, hipStream_t stream, size_t smem) {
-  const void* fn = (const void*)render_basic_kernel<CULL, COUNT, LDS, HYB, HEAVY, SPLIT, C16>;
+  const void* fn = (const void*)render_basic_kernel<CULL, COUNT, LDS, HYB, HEAVY, SPLIT, C16, PACKET>;
   const int block = basic_block_threads<LDS, sphere_waves<HEAVY>()>();
   /* LDS: the staged scene, then one u32 result slot per thread (layout.h LDS_SCENE_MAX_BYTES leaves
    * room for both, twice per CU) */
@@ -282,7 +324,7 @@ void launch_basic(const KParams& kp, int device, hipStream_t stream, size_t smem
   p.lane_lds = LDS ? (uint32_t)((smem + 15) & ~(size_t)15) : 0u;
   const size_t total = p.lane_lds + (size_t)block * sizeof(uint32_t);
   const int grid = resident_grid(fn, block, device, total, true, __PRETTY_FUNCTION__);
-  hipLaunchKernelGGL((render_basic_kernel<CULL, COUNT, LDS, HYB, HEAVY, SPLIT, C16>), dim3(grid), dim3(block), total, stream, p);
+  hipLaunchKernelGGL((render_basic_kernel<CULL, COUNT, LDS, HYB, HEAVY, SPLIT, C16, PACKET>), dim3(grid), dim3(block), total, stream, p);
   hip_check(hipGetLastError(), "render_basic_kernel launch");
 }
 
@@ -291,8 +333,15 @@ void launch_basic(const KParams& kp, int device, hipStream_t stream, size_t smem
 
 namespace hrt {
 
-void launch_sphere(int cull, bool count, bool lds, bool heavy, const KParams& kp, int device, hipStream_t stream,
+void launch_sphere(int cull, bool count, bool lds, bool heavy, bool packet, const KParams& kp, int device, hipStream_t stream,
                    size_t smem) {
+  if (packet && lds && cull == G::CULL_EXACT && kp.walk_hot == 0 && kp.walk_half == 16u && !kp.walk_c16) {
+    if (heavy) count ? launch_basic<G::CULL_EXACT, true, true, false, true, false, false, true>(kp, device, stream, smem)
+                     : launch_basic<G::CULL_EXACT, false, true, false, true, false, false, true>(kp, device, stream, smem);
+    else count ? launch_basic<G::CULL_EXACT, true, true, false, false, false, false, true>(kp, device, stream, smem)
+               : launch_basic<G::CULL_EXACT, false, true, false, false, false, false, true>(kp, device, stream, smem);
+    return;
+  }
   if (heavy) { /* noise / image textures (exact culling only: plan()) */
     if (lds && kp.walk_hot > 0) { /* a stream beyond the LDS budget: its staged part in LDS, the rest global */
       count ? launch_basic<G::CULL_EXACT, true, true, true, true>(kp, device, stream, smem)
