@@ -7,6 +7,7 @@
 #     "smoke"                                    __graft_entry__.smoke()                        -> smoke.log
 #     "bench <tag> [bench args]"                 one bench.py line                              -> <tag>.jsonl
 #     "rehearsal <tag> [bench args]"             2 ranks sharing GPU 0 (--one-device)           -> <tag>.jsonl
+#     "rehearsaln <tag> <N> [bench args]"        N ranks (N <= 4) sharing GPU 0 (--one-device)  -> <tag>.jsonl
 #     "rehtrace <tag> [bench args]"              the same under rocprofv3 --kernel-trace         -> prof_<tag>/
 #     "configs <tag>"                            BASELINE configs 3-5 lines (C4 / C5 also as an 8-way share)
 #     "profile <tag> <preset> <W> <H> <spp> [share] [bench args]"
@@ -82,6 +83,12 @@ step() {
       local tag=$1; shift
       echo "== $tag: 2-rank rehearsal $*" >> "$LOG"
       timeout -k 10 240 python -u bench.py --gpus 2 --one-device "$@" >> "$OUT/$tag.jsonl" 2>> "$OUT/$tag.err"
+      local rc=$?; echo "== $tag exit $rc" >> "$LOG"; return $rc ;;
+    rehearsaln)  # N ranks on one GPU (the N > 1 code paths: split, delivery, parity and CPU leg on the N-GPU frame)
+      local tag=$1 n=$2; shift 2
+      [ "$n" -le 4 ] || { echo "rehearsaln: at most 4 ranks" >> "$LOG"; return 2; }
+      echo "== $tag: $n-rank rehearsal $*" >> "$LOG"
+      timeout -k 10 400 python -u bench.py --gpus "$n" --one-device "$@" >> "$OUT/$tag.jsonl" 2>> "$OUT/$tag.err"
       local rc=$?; echo "== $tag exit $rc" >> "$LOG"; return $rc ;;
     rehtrace)  # kernel timeline of a concurrent 2-rank rehearsal: one rocprofv3 per rank (each rank its own
       # profiled program with the process-group variables set, so bench.py never spawns under the profiler's preload)
