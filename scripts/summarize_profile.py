@@ -147,7 +147,7 @@ def main():
     if launch:
         res["launch"] = launch
         res["dispatch_ordinal"] = ordinal
-        lines.append(f"\n**Launch** (hrt_last_launch): `{launch['kernel'][:120]}`, grid {launch['grid']} x {launch['block']} "
+        lines.append(f"\n**Launch** (hrt_last_launch): `{launch['kernel']}`, grid {launch['grid']} x {launch['block']} "
                      f"({launch['blocks_per_cu']} workgroups per CU x {launch['cus']} CUs, {launch['waves_per_simd']} waves/SIMD), "
                      f"{launch['vgprs']} VGPRs, {launch['scratch_bytes']} B scratch per lane, {launch['lds_bytes']} B LDS")
         if "SQ_WAVES" in c and int(round(c["SQ_WAVES"])) != want:
