@@ -282,3 +282,75 @@ def test_final_scene_draws_and_structure_restated_independently():
     pm = pt[4096:].view(np.uint32).reshape(3, 256)
     assert all(_same(rv[i][j], ranvec[i][j]) for i in range(256) for j in range(3))
     assert [list(map(int, pm[c])) for c in range(3)] == perms
+
+
+# ------------------------------------------------------------------------------- application.rs:639-721 (Cornell)
+def rect_box(r):  # rect.rs:88-102 (the ZX box transposed relative to its hit test: G17, kept)
+    plane, a0, a1, b0, b1, k = r
+    e = f(0.0001)
+    if plane == 0:
+        return (a0, b0, k - e), (a1, b1, k + e)
+    if plane == 1:
+        return (k - e, a0, b0), (k + e, a1, b1)
+    return (a0, k - e, b0), (a1, k + e, b1)
+
+
+def rotated_box(box, axis, angle):  # rotation.rs:38-90: the eight corners turned, f32 sin / cos of the angle
+    import math
+
+    r_axis, a_axis, b_axis = {0: (0, 1, 2), 1: (1, 2, 0), 2: (2, 0, 1)}[axis]
+    radians = (f(math.pi) / f(180.0)) * f(angle)  # (PI / 180.0) * angle, std::f32::consts::PI
+    sin_t, cos_t = f(math.sin(float(radians))), f(math.cos(float(radians)))
+    mn = [f(np.finfo(np.float32).max)] * 3
+    mx = [f(-np.finfo(np.float32).max)] * 3
+    for i in range(2):
+        for j in range(2):
+            for k in range(2):
+                r = f(k) * box[1][r_axis] + f(1 - k) * box[0][r_axis]
+                a = f(i) * box[1][a_axis] + f(1 - i) * box[0][a_axis]
+                b = f(j) * box[1][b_axis] + f(1 - j) * box[0][b_axis]
+                na = cos_t * a - sin_t * b
+                nb = sin_t * a + cos_t * b
+                mn[a_axis], mn[b_axis], mn[r_axis] = min(mn[a_axis], na), min(mn[b_axis], nb), min(mn[r_axis], r)
+                mx[a_axis], mx[b_axis], mx[r_axis] = max(mx[a_axis], na), max(mx[b_axis], nb), max(mx[r_axis], r)
+    return tuple(mn), tuple(mx)
+
+
+def test_cornell_scene_structure_restated_independently():
+    """Cornell (application.rs:639-721): five walls and the light as Rects, two Cuboids each in a Rotation (Y, 15
+    and -18 degrees) inside a Translation, all under one BvhNode (its sort keys from rect.rs's boxes, the rotated
+    corners of rotation.rs and translation.rs's offset): the library's primitives in that pre-order, the walls at
+    world level with their materials, each cuboid's six sides in its own frame, bit for bit."""
+    prims, mats, texs, info = _records("cornell")
+    pu = prims.view(np.uint32)
+    red, white, green = v3(0.65, 0.05, 0.05), v3(0.73, 0.73, 0.73), v3(0.12, 0.45, 0.15)
+    F = lambda *x: tuple(f(v) for v in x)  # noqa: E731
+    objs = [("rect", F(1, 0, 555, 0, 555, 555), green), ("rect", F(1, 0, 555, 0, 555, 0), red),
+            ("rect", F(2, 213, 343, 227, 332, 554), "light"), ("rect", F(2, 0, 555, 0, 555, 0), white),
+            ("rect", F(2, 0, 555, 0, 555, 555), white), ("rect", F(0, 0, 555, 0, 555, 555), white)]
+    for size, angle, off in ((v3(165, 330, 165), 15.0, v3(265, 0, 295)), (v3(165, 165, 165), -18.0, v3(130, 0, 65))):
+        cb = (v3(0, 0, 0), size)
+        rb = rotated_box(cb, 1, angle)
+        objs.append(("box", cb, (vadd(rb[0], off), vadd(rb[1], off))))
+
+    def box(o, t0, t1):
+        return rect_box(o[1]) if o[0] == "rect" else o[2]
+    leaves = bvh_leaves(objs, box=box)
+    want = []
+    for o in leaves:
+        if o[0] == "rect":
+            want.append((o[1], o[2], True))
+        else:
+            want += [(tuple(f(v) for v in r), white, False) for r in cuboid_rects(*o[1])]
+    assert len(want) == len(prims) == 18
+    for k, (r, mat, world) in enumerate(want):
+        p = prims[k]
+        assert (pu[k, 11] & 3) == 2 and ((pu[k, 11] >> 2) & 3) == int(r[0]), k
+        assert all(_same(p[j], r[1 + j]) for j in range(4)) and _same(p[4], r[5]), (k, p[:5], r)
+        assert (pu[k, 10] == 0xFFFFFFFF) == world, k
+        m = mats[pu[k, 11] >> 4]
+        t = texs[_u(m[5])]
+        if mat == "light":
+            assert _u(m[4]) == 3 and all(_same(t[j], 15.0) for j in range(3))
+        else:
+            assert _u(m[4]) == 0 and all(_same(t[j], mat[j]) for j in range(3)), k
