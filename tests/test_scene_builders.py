@@ -354,3 +354,31 @@ def test_cornell_scene_structure_restated_independently():
             assert _u(m[4]) == 3 and all(_same(t[j], 15.0) for j in range(3))
         else:
             assert _u(m[4]) == 0 and all(_same(t[j], mat[j]) for j in range(3)), k
+
+
+@pytest.mark.parametrize("name", ["two_perlin_spheres", "earth_perlin", "simple_light"])
+def test_noise_scenes_restated_independently(name):
+    """The Perlin scenes (application.rs:589-602, :614-637, and config 3's Earth over that ground): the noise
+    texture's tables drawn first from the scene stream (perlin_noise.rs:28-45, the thread_rng substitution), the
+    ground sphere and the small sphere under one BvhNode (the ground first on the y axis), with NoiseTexture's
+    scale 4: the library's records bit for bit."""
+    prims, mats, texs, info = _records(name)
+    pu = prims.view(np.uint32)
+    ranvec, perms = K.perlin_tables(K.scene_rng(1))
+    b = np.frombuffer(hrt.scene_blob(hrt.preset(name, 1))[0].raw, np.uint8)
+    pt = b[info.off_perlin:info.off_perlin + 7168]
+    rv = pt[:4096].view(np.float32).reshape(256, 4)
+    pm = pt[4096:].view(np.uint32).reshape(3, 256)
+    assert all(_same(rv[i][j], ranvec[i][j]) for i in range(256) for j in range(3))
+    assert [list(map(int, pm[c])) for c in range(3)] == perms
+    objs = [("sphere", v3(0, -1000, 0), None, f(1000), "noise"),
+            ("sphere", v3(0, 2, 0), None, f(2), "image" if name == "earth_perlin" else "noise")]
+    spheres = [p for p in range(len(prims)) if (pu[p, 11] & 3) == 0]
+    for k, o in zip(spheres, bvh_leaves(objs)):
+        assert all(_same(prims[k][j], o[1][j]) for j in range(3)) and _same(prims[k][3], o[3])
+        t = texs[_u(mats[pu[k, 11] >> 4][5])]
+        if o[4] == "noise":
+            assert _u(t[4]) == 2 and _same(t[0], 4.0)
+        else:
+            assert _u(t[4]) == 3
+    assert len(spheres) == 2
