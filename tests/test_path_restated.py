@@ -1,0 +1,180 @@
+"""The whole per-pixel path of the headline scene restated a third time, in Python, from the Rust sources, and held
+bit for bit to the CPU oracle (which the GPU is held to by tests/test_gpu_parity.py and bench.py's parity band).
+
+The oracle (oracle/oracle.cpp) and the library (csrc/lane.h) share include/hrt/hd_math.h, so a misreading of the
+path itself -- the sample loop's draw order (application.rs:443-453), Camera::get_ray (camera.rs:85-95),
+BvhNode::hit's left-then-right walk with the shrinking t_max (bvh_node.rs:104-127), ray_color's recursion
+(application.rs:477-495), the materials' scatter and their draws (lambertian.rs:27-38, metal.rs:29-42,
+dielectric.rs:31-55), the checker texture -- would be shared by both.  This test restates that path on numpy
+float32 scalars (one IEEE rounding per operation, cgmath's operation order) with the unit functions of the KAT
+generator (tests/golden/make_kats.py: aabb.rs, sphere.rs, moving_sphere.rs, camera.rs, math.rs, checker_texture.rs,
+the seeded per-sample RNG with rand 0.8.5's transforms) and the scene of tests/test_scene_builders.py (which is
+held to the library's lowered scene), renders a few pixels of the Random scene, and compares colour and world.hit
+count with the oracle's render of the same pixels: equal bits, equal counts.  Parity against the reference binary
+stays unpinned (it cannot run here); this pins the C++ restatements against an independent reading."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import hrt
+from oracle import oracle as O
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import test_scene_builders as SB  # noqa: E402
+
+K = SB.K
+f = np.float32
+INF = f(np.inf)
+
+
+class Bvh:
+    """BvhNode::new's tree (bvh_node.rs:27-63) over the scene's objects, with each node's box."""
+
+    def __init__(self, objs, t0=0.0, t1=1.0):
+        objs = list(objs)
+        ranges = []
+        for axis in range(3):
+            mn, mx = f(np.finfo(np.float32).max), f(np.finfo(np.float32).min)
+            for o in objs:
+                b = SB.bbox(o, t0, t1)
+                mn, mx = min(mn, b[0][axis]), max(mx, b[1][axis])
+            ranges.append((axis, mx - mn))
+        ranges.sort(key=lambda ar: -ar[1])
+        axis = ranges[0][0]
+        objs.sort(key=lambda o: SB.bbox(o, t0, t1)[0][axis] + SB.bbox(o, t0, t1)[1][axis])
+        if len(objs) == 1:
+            self.leaf, self.left, self.right = objs[0], None, None
+            self.box = SB.bbox(objs[0], t0, t1)
+            return
+        half = len(objs) // 2
+        self.leaf = None
+        self.right = Bvh(objs[half:], t0, t1)
+        self.left = Bvh(objs[:half], t0, t1)
+        self.box = SB.surrounding(self.left.box, self.right.box)
+
+    def hit(self, o, d, time, tmin, tmax):
+        """BvhNode::hit (bvh_node.rs:104-127): the box, then the left child, the right one with t_max shrunk."""
+        if not K.aabb_hit(self.box[0], self.box[1], o, d, tmin, tmax):
+            return None
+        if self.leaf is not None:
+            kind, c0, c1, r, mat = self.leaf
+            c = c0 if kind == "sphere" else K.moving_center(c0, c1, f(0), f(1), time)  # moving_sphere.rs:53-58
+            h = K.sphere_hit(c, r, o, d, tmin, tmax)
+            return None if h is None else (h, mat)
+        left = self.left.hit(o, d, time, tmin, tmax)
+        right = self.right.hit(o, d, time, tmin, left[0][0] if left is not None else tmax)
+        return right if right is not None else left
+
+
+def random_in_unit_sphere(rng):  # math.rs:16-30 (Uniform(-1, 1): the gen_range bits, no retry needed)
+    while True:
+        p = (rng.gen_range(-1.0, 1.0), rng.gen_range(-1.0, 1.0), rng.gen_range(-1.0, 1.0))
+        if K.dot(p, p) < f(1):
+            return p
+
+
+def random_in_unit_disk(rng):  # math.rs:32-40
+    while True:
+        p = (rng.gen_range(-1.0, 1.0), rng.gen_range(-1.0, 1.0), f(0))
+        if K.dot(p, p) < f(1):
+            return p
+
+
+def scatter(mat, rng, d, rec):
+    """(attenuation, direction) or None (materials/*.rs scatter)."""
+    t, px, py, pz, nx, ny, nz, u, v, front = rec
+    p, n = (px, py, pz), (nx, ny, nz)
+    kind = mat[0]
+    if kind in ("lambertian", "lambertian_checker"):  # lambertian.rs:27-38
+        sd = K.add(n, K.norm(random_in_unit_sphere(rng)))
+        if K.near_zero(sd):
+            sd = n
+        att = mat[1] if kind == "lambertian" else (mat[1] if K.checker(p) == K.F3((0.2, 0.3, 0.1)) else mat[2])
+        return att, sd
+    if kind == "metal":  # metal.rs:29-42
+        refl = K.reflect(K.norm(d), n)
+        sd = K.add(refl, K.smul(mat[2], random_in_unit_sphere(rng)))
+        return (mat[1], sd) if K.dot(sd, n) > f(0) else None
+    ratio = (f(1) / mat[1]) if front else mat[1]  # dielectric.rs:31-55
+    ud = K.norm(d)
+    cos_t = min(K.dot(K.neg(ud), n), f(1))
+    sin_t = np.sqrt(f(1) - cos_t * cos_t)
+    if (ratio * sin_t) > f(1) or K.reflectance(cos_t, ratio) > rng.gen_f32():
+        sd = K.reflect(ud, n)
+    else:
+        sd = K.refract(ud, n, ratio)
+    return (f(1), f(1), f(1)), sd
+
+
+def ray_color(world, o, d, time, background, depth, rng, count):
+    """application.rs:477-495, recursive as the reference is."""
+    if depth == 0:
+        return (f(0), f(0), f(0))
+    count[0] += 1
+    h = world.hit(o, d, time, f(0.001), INF)
+    if h is None:
+        return background
+    rec, mat = h
+    s = scatter(mat, rng, d, rec)
+    emitted = (f(0), f(0), f(0))
+    if s is None:
+        return emitted
+    att, sd = s
+    col = ray_color(world, (rec[1], rec[2], rec[3]), sd, time, background, depth - 1, rng, count)
+    return K.add((att[0] * col[0], att[1] * col[1], att[2] * col[2]), emitted)
+
+
+def render_pixel(world, cam, bg, W, H, x, y, spp, depth, seed, count):
+    """The sample loop (application.rs:443-456) for one pixel: each sample on its own keyed stream (the thread_rng
+    substitution), u and v jitter, Camera::get_ray (lens disk, then the shutter time), the colours summed."""
+    total = (f(0), f(0), f(0))
+    for s in range(spp):
+        rng = K.Rng(K.path_key(seed, y * W + x, s))
+        u = (f(x) + rng.gen_f32()) / (f(W) - f(1))
+        v = (f(y) + rng.gen_f32()) / (f(H) - f(1))
+        disk = random_in_unit_disk(rng)
+        time = rng.gen_range(0.0, 1.0)
+        r = K.camera_ray(cam, u, v, disk, time)
+        total = K.add(total, ray_color(world, tuple(r[0:3]), tuple(r[3:6]), r[6], bg, depth, rng, count))
+    scale = f(1) / f(spp)
+    return tuple(np.sqrt(c * scale) for c in total)
+
+
+@pytest.mark.parametrize("x,y", [(20, 10), (45, 22), (5, 30), (33, 17), (60, 2), (31, 12)])
+def test_random_scene_path_equals_oracle_bit_for_bit(x, y):
+    """Pixels of the Random scene at 64 x 36, 16 spp, depth 50 (spheres, moving spheres, Lambertian solid and
+    checker, Metal, Dielectric): the restated path's colour and world.hit count equal the oracle's exactly."""
+    W, H, spp, depth, seed = 64, 36, 16, 50, 3
+    s = hrt.preset("random", 1)
+    info = s.info
+    world = Bvh(SB.random_scene(K.scene_rng(1)))
+    cam = K.camera(K.F3(info.look_from), K.F3(info.look_at), f(info.fov), f(info.aperture), f(info.focus_dist), W, H)
+    bg = K.F3(info.background)
+    count = [0]
+    got = render_pixel(world, cam, bg, W, H, x, y, spp, depth, seed, count)
+    ref, cnt = O.OracleScene(hrt.PRESETS["random"], 1).render(W, H, spp, depth, seed=seed, region=(x, y, 1, 1), threads=1)
+    assert count[0] == cnt["segments"], (count[0], cnt["segments"])
+    for c in range(3):
+        assert np.float32(got[c]).view(np.uint32) == np.float32(ref[0, 0, c]).view(np.uint32), (c, got, ref[0, 0, :3])
+
+
+def test_restated_path_has_teeth():
+    """One misreading in the sample loop (v's jitter drawn before u's) changes the restated pixel: the equality
+    above is not a comparison that anything passes."""
+    W, H, spp, depth, seed, x, y = 64, 36, 16, 50, 3, 33, 17
+    info = hrt.preset("random", 1).info
+    world = Bvh(SB.random_scene(K.scene_rng(1)))
+    cam = K.camera(K.F3(info.look_from), K.F3(info.look_at), f(info.fov), f(info.aperture), f(info.focus_dist), W, H)
+    bg = K.F3(info.background)
+    good = render_pixel(world, cam, bg, W, H, x, y, spp, depth, seed, [0])
+    total = (f(0), f(0), f(0))
+    for s in range(spp):
+        rng = K.Rng(K.path_key(seed, y * W + x, s))
+        v = (f(y) + rng.gen_f32()) / (f(H) - f(1))
+        u = (f(x) + rng.gen_f32()) / (f(W) - f(1))
+        r = K.camera_ray(cam, u, v, random_in_unit_disk(rng), rng.gen_range(0.0, 1.0))
+        total = K.add(total, ray_color(world, tuple(r[0:3]), tuple(r[3:6]), r[6], bg, depth, rng, [0]))
+    bad = tuple(np.sqrt(c * (f(1) / f(spp))) for c in total)
+    assert good != bad
