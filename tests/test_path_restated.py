@@ -9,8 +9,10 @@ dielectric.rs:31-55), the checker texture -- would be shared by both.  This test
 float32 scalars (one IEEE rounding per operation, cgmath's operation order) with the unit functions of the KAT
 generator (tests/golden/make_kats.py: aabb.rs, sphere.rs, moving_sphere.rs, camera.rs, math.rs, checker_texture.rs,
 the seeded per-sample RNG with rand 0.8.5's transforms) and the scene of tests/test_scene_builders.py (which is
-held to the library's lowered scene), renders a few pixels of the Random scene, and compares colour and world.hit
-count with the oracle's render of the same pixels: equal bits, equal counts.  Parity against the reference binary
+held to the library's lowered scene), renders a few pixels of the Random scene (configs 1-2) and of Cornell (config
+5: rect.rs, list.rs, rotation.rs -- whose hit turns the normal back without set_face_normal -- translation.rs,
+diffuse_light.rs), and compares colour and world.hit count with the oracle's render of the same pixels: equal
+bits, equal counts.  Parity against the reference binary
 stays unpinned (it cannot run here); this pins the C++ restatements against an independent reading."""
 import os
 import sys
@@ -178,3 +180,165 @@ def test_restated_path_has_teeth():
         total = K.add(total, ray_color(world, tuple(r[0:3]), tuple(r[3:6]), r[6], bg, depth, rng, [0]))
     bad = tuple(np.sqrt(c * (f(1) / f(spp))) for c in total)
     assert good != bad
+
+
+# ------------------------------------------------------------------------------- Cornell (application.rs:639-721)
+class Rect:  # rect.rs:53-102
+    def __init__(self, r, mat):
+        self.r, self.mat = r, mat
+
+    def box(self):
+        return SB.rect_box(self.r)
+
+    def hit(self, o, d, time, tmin, tmax):
+        h = K.rect_hit(*self.r, o, d, tmin, tmax)
+        return None if h is None else (h, self.mat)
+
+
+class HList:  # list.rs:20-31 (a Cuboid's sides, cuboid.rs)
+    def __init__(self, items):
+        self.items = items
+
+    def hit(self, o, d, time, tmin, tmax):
+        closest, best = tmax, None
+        for it in self.items:
+            h = it.hit(o, d, time, tmin, closest)
+            if h is not None:
+                closest, best = h[0][0], h
+        return best
+
+
+class Rotate:  # rotation.rs:38-134 (the normal turned back, no set_face_normal)
+    def __init__(self, axis, child, angle, child_box):
+        import math
+
+        self.child = child
+        _, self.a, self.b = {0: (0, 1, 2), 1: (1, 2, 0), 2: (2, 0, 1)}[axis]
+        radians = (f(math.pi) / f(180.0)) * f(angle)
+        self.s, self.c = f(math.sin(float(radians))), f(math.cos(float(radians)))
+        self.bx = SB.rotated_box(child_box, axis, angle)
+
+    def box(self):
+        return self.bx
+
+    def hit(self, o, d, time, tmin, tmax):
+        a, b, s, c = self.a, self.b, self.s, self.c
+        o2, d2 = list(o), list(d)
+        o2[a], o2[b] = c * o[a] + s * o[b], -s * o[a] + c * o[b]
+        d2[a], d2[b] = c * d[a] + s * d[b], -s * d[a] + c * d[b]
+        h = self.child.hit(tuple(o2), tuple(d2), time, tmin, tmax)
+        if h is None:
+            return None
+        rec, mat = h
+        p, n = list(rec[1:4]), list(rec[4:7])
+        p[a], p[b] = c * rec[1 + a] - s * rec[1 + b], s * rec[1 + a] + c * rec[1 + b]
+        n[a], n[b] = c * rec[4 + a] - s * rec[4 + b], s * rec[4 + a] + c * rec[4 + b]
+        return [rec[0], *p, *n, *rec[7:]], mat
+
+
+class Translate:  # translation.rs:24-47
+    def __init__(self, child, off):
+        self.child, self.off = child, off
+
+    def box(self):
+        b = self.child.box()
+        return SB.vadd(b[0], self.off), SB.vadd(b[1], self.off)
+
+    def hit(self, o, d, time, tmin, tmax):
+        mo = SB.vsub(o, self.off)
+        h = self.child.hit(mo, d, time, tmin, tmax)
+        if h is None:
+            return None
+        rec, mat = h
+        front, n = K.face(d, tuple(rec[4:7]))  # set_face_normal(moved_ray, normal)
+        return [rec[0], *SB.vadd(tuple(rec[1:4]), self.off), *n, rec[7], rec[8], f(1) if front else f(0)], mat
+
+
+class Bvh2:
+    """BvhNode::new / ::hit over objects with box() and hit() (bvh_node.rs:27-127)."""
+
+    def __init__(self, idx, objs):
+        ranges = []
+        for axis in range(3):
+            mn, mx = f(np.finfo(np.float32).max), f(np.finfo(np.float32).min)
+            for i in idx:
+                b = objs[i].box()
+                mn, mx = min(mn, b[0][axis]), max(mx, b[1][axis])
+            ranges.append((axis, mx - mn))
+        ranges.sort(key=lambda ar: -ar[1])
+        axis = ranges[0][0]
+        idx = sorted(idx, key=lambda i: objs[i].box()[0][axis] + objs[i].box()[1][axis])
+        if len(idx) == 1:
+            self.leaf, self.bx = objs[idx[0]], objs[idx[0]].box()
+            return
+        half = len(idx) // 2
+        self.leaf = None
+        self.right, self.left = Bvh2(idx[half:], objs), Bvh2(idx[:half], objs)
+        self.bx = SB.surrounding(self.left.bx, self.right.bx)
+
+    def hit(self, o, d, time, tmin, tmax):
+        if not K.aabb_hit(self.bx[0], self.bx[1], o, d, tmin, tmax):
+            return None
+        if self.leaf is not None:
+            return self.leaf.hit(o, d, time, tmin, tmax)
+        left = self.left.hit(o, d, time, tmin, tmax)
+        right = self.right.hit(o, d, time, tmin, left[0][0] if left is not None else tmax)
+        return right if right is not None else left
+
+
+def cornell_world():
+    red, white, green = ("lambertian", SB.v3(0.65, 0.05, 0.05)), ("lambertian", SB.v3(0.73, 0.73, 0.73)), \
+        ("lambertian", SB.v3(0.12, 0.45, 0.15))
+    light = ("light", SB.v3(15, 15, 15))
+    F = lambda *x: tuple(f(v) for v in x)  # noqa: E731
+    objs = [Rect(F(1, 0, 555, 0, 555, 555), green), Rect(F(1, 0, 555, 0, 555, 0), red),
+            Rect(F(2, 213, 343, 227, 332, 554), light), Rect(F(2, 0, 555, 0, 555, 0), white),
+            Rect(F(2, 0, 555, 0, 555, 555), white), Rect(F(0, 0, 555, 0, 555, 555), white)]
+    for size, angle, off in ((SB.v3(165, 330, 165), 15.0, SB.v3(265, 0, 295)), (SB.v3(165, 165, 165), -18.0, SB.v3(130, 0, 65))):
+        sides = HList([Rect(tuple(f(v) for v in r), white) for r in SB.cuboid_rects(SB.v3(0, 0, 0), size)])
+        objs.append(Translate(Rotate(1, sides, angle, (SB.v3(0, 0, 0), size)), off))
+    return Bvh2(list(range(len(objs))), objs)
+
+
+def ray_color_full(world, o, d, time, background, depth, rng, count):
+    """application.rs:477-495 with emission (DiffuseLight: no scatter, emitted = its colour, diffuse_light.rs)."""
+    if depth == 0:
+        return (f(0), f(0), f(0))
+    count[0] += 1
+    h = world.hit(o, d, time, f(0.001), INF)
+    if h is None:
+        return background
+    rec, mat = h
+    if mat[0] == "light":
+        return mat[1]
+    s = scatter(mat, rng, d, rec)
+    if s is None:
+        return (f(0), f(0), f(0))
+    att, sd = s
+    col = ray_color_full(world, (rec[1], rec[2], rec[3]), sd, time, background, depth - 1, rng, count)
+    return K.add((att[0] * col[0], att[1] * col[1], att[2] * col[2]), (f(0), f(0), f(0)))
+
+
+@pytest.mark.parametrize("x,y", [(20, 10), (30, 12), (8, 30), (25, 5), (14, 20)])
+def test_cornell_path_equals_oracle_bit_for_bit(x, y):
+    """Pixels of Cornell (config 5's scene) at 40 x 40, 24 spp: the restated path -- Rects (rect.rs), the cuboids'
+    sides as Lists, Rotation without set_face_normal and Translation with it, the light's emission -- equals the
+    oracle's colours and world.hit counts exactly."""
+    W, H, spp, depth, seed = 40, 40, 24, 50, 5
+    info = hrt.preset("cornell", 1).info
+    world = cornell_world()
+    cam = K.camera(K.F3(info.look_from), K.F3(info.look_at), f(info.fov), f(info.aperture), f(info.focus_dist), W, H)
+    bg = K.F3(info.background)
+    count = [0]
+    total = (f(0), f(0), f(0))
+    for s in range(spp):
+        rng = K.Rng(K.path_key(seed, y * W + x, s))
+        u = (f(x) + rng.gen_f32()) / (f(W) - f(1))
+        v = (f(y) + rng.gen_f32()) / (f(H) - f(1))
+        r = K.camera_ray(cam, u, v, random_in_unit_disk(rng), rng.gen_range(float(info.time0), float(info.time1)))
+        total = K.add(total, ray_color_full(world, tuple(r[0:3]), tuple(r[3:6]), r[6], bg, depth, rng, count))
+    got = tuple(np.sqrt(c * (f(1) / f(spp))) for c in total)
+    ref, cnt = O.OracleScene(hrt.PRESETS["cornell"], 1).render(W, H, spp, depth, seed=seed, region=(x, y, 1, 1), threads=1)
+    assert count[0] == cnt["segments"], (count[0], cnt["segments"])
+    for c in range(3):
+        assert np.float32(got[c]).view(np.uint32) == np.float32(ref[0, 0, c]).view(np.uint32), (c, got, ref[0, 0, :3])
