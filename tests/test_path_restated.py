@@ -342,3 +342,151 @@ def test_cornell_path_equals_oracle_bit_for_bit(x, y):
     assert count[0] == cnt["segments"], (count[0], cnt["segments"])
     for c in range(3):
         assert np.float32(got[c]).view(np.uint32) == np.float32(ref[0, 0, c]).view(np.uint32), (c, got, ref[0, 0, :3])
+
+
+# ------------------------------------------------------------------------------- Final (application.rs:817-935)
+class Sphere:  # sphere.rs / moving_sphere.rs (a moving one when c1 is given, over the shutter [0, 1])
+    def __init__(self, c0, r, mat, c1=None):
+        self.c0, self.c1, self.r, self.mat = c0, c1, f(r), mat
+
+    def centre(self, time):
+        return self.c0 if self.c1 is None else K.moving_center(self.c0, self.c1, f(0), f(1), time)
+
+    def box(self):
+        if self.c1 is None:
+            return SB.sphere_box(self.c0, self.r)
+        return SB.surrounding(SB.sphere_box(self.centre(f(0)), self.r), SB.sphere_box(self.centre(f(1)), self.r))
+
+    def hit(self, o, d, time, tmin, tmax):
+        h = K.sphere_hit(self.centre(time), self.r, o, d, tmin, tmax)
+        return None if h is None else (h, self.mat)
+
+
+class Cuboid(HList):  # cuboid.rs: its six sides as a List, its box (box_min, box_max)
+    def __init__(self, p0, p1, mat):
+        super().__init__([Rect(r, mat) for r in SB.cuboid_rects(p0, p1)])
+        self.bx = (p0, p1)
+
+    def box(self):
+        return self.bx
+
+
+class Medium:  # constant_medium.rs:34-76; the draw keyed by (path, segment, medium id): hd_math.h medium_xi
+    def __init__(self, boundary, density, albedo, medium_id):
+        self.boundary, self.nid, self.mat, self.id = boundary, f(-1.0) / f(density), ("isotropic", albedo), medium_id
+
+    def box(self):
+        return self.boundary.box()
+
+    def hit(self, o, d, time, tmin, tmax, key=None):
+        r1 = self.boundary.hit(o, d, time, -INF, INF)
+        if r1 is None:
+            return None
+        r2 = self.boundary.hit(o, d, time, r1[0][0] + f(0.0001), INF)
+        if r2 is None:
+            return None
+        t1, t2 = r1[0][0], r2[0][0]
+        t1 = tmin if t1 < tmin else t1
+        t2 = tmax if t2 > tmax else t2
+        if t1 >= t2:
+            return None
+        t1 = f(0) if t1 < f(0) else t1
+        length = np.sqrt(K.dot(d, d))
+        inside = (t2 - t1) * length
+        pkey, segment = PATH[0], PATH[1]
+        k = K.mix64(pkey ^ K.mix64(0xC2B2AE3D27D4EB4F ^ ((segment << 32) | self.id)))
+        xi = f((k >> 32) >> 8) * f(2.0 ** -24)
+        hit_distance = self.nid * (f(np.log(np.float64(xi))) / f(np.log(np.float64(f(np.e)))))
+        if hit_distance > inside:
+            return None
+        t = t1 + hit_distance / length
+        return [t, *K.at(o, d, t), f(0), f(0), f(0), f(0), f(0), f(0)], self.mat
+
+
+PATH = [0, 0]  # the current sample's path key and segment index (the medium draw's key)
+
+
+def final_world(earth):
+    ground, (ranvec, perms), centres = SB.final_draws(K.scene_rng(1))
+    green = ("lambertian", SB.v3(0.48, 0.83, 0.53))
+    objs = [Bvh2(list(range(400)), [Cuboid(p0, p1, green) for p0, p1 in ground])]
+    F = lambda *x: tuple(f(v) for v in x)  # noqa: E731
+    objs.append(Rect(F(2, 123, 423, 147, 412, 554), ("light", SB.v3(7, 7, 7))))
+    objs.append(Sphere(SB.v3(400, 400, 200), 50, ("lambertian", SB.v3(0.7, 0.3, 0.1)), c1=SB.vadd(SB.v3(400, 400, 200), SB.v3(30, 0, 0))))
+    objs.append(Sphere(SB.v3(260, 150, 45), 50, ("dielectric", f(1.5))))
+    objs.append(Sphere(SB.v3(0, 150, 145), 50, ("metal", SB.v3(0.8, 0.8, 0.9), f(1.0))))
+    objs.append(Sphere(SB.v3(360, 150, 145), 70, ("dielectric", f(1.5))))
+    objs.append(Medium(Sphere(SB.v3(360, 150, 145), 70, ("dielectric", f(1.5))), 0.2, SB.v3(0.2, 0.4, 0.9), 0))
+    objs.append(Medium(Sphere(SB.v3(0, 0, 0), 5000, ("dielectric", f(1.5))), 0.0001, SB.v3(1, 1, 1), 1))
+    objs.append(Sphere(SB.v3(400, 200, 400), 100, ("image", earth)))
+    objs.append(Sphere(SB.v3(220, 280, 300), 80, ("noise", f(0.1), ranvec, perms)))
+    white = ("lambertian", SB.v3(0.73, 0.73, 0.73))
+    inner = Bvh2(list(range(1000)), [Sphere(c, 10, white) for c in centres])
+    inner.box = lambda: inner.bx
+    objs.append(Translate(Rotate(1, inner, 15.0, inner.bx), SB.v3(-100, 270, 395)))
+    for o in objs:
+        if isinstance(o, Bvh2):
+            o.box = (lambda b: (lambda: b))(o.bx)
+    return Bvh2(list(range(len(objs))), objs)
+
+
+def shade_final(mat, rng, d, rec):
+    """(attenuation, direction) or None, with the Next-Week materials and textures (noise_texture.rs:24-31,
+    image_texture.rs:36-62, isotropic.rs:26-33)."""
+    p = tuple(rec[1:4])
+    if mat[0] == "image":
+        return K.image_tex(mat[1], rec[7], rec[8]), scatter(("lambertian", (f(0), f(0), f(0))), rng, d, rec)[1]
+    if mat[0] == "noise":
+        att = K.noise_tex(mat[2], mat[3], mat[1], p)
+        return att, scatter(("lambertian", (f(0), f(0), f(0))), rng, d, rec)[1]
+    if mat[0] == "isotropic":
+        return mat[1], random_in_unit_sphere(rng)
+    return scatter(mat, rng, d, rec)
+
+
+def ray_color_final(world, o, d, time, background, depth, rng, count):
+    if depth == 0:
+        return (f(0), f(0), f(0))
+    count[0] += 1
+    h = world.hit(o, d, time, f(0.001), INF)
+    PATH[1] += 1
+    if h is None:
+        return background
+    rec, mat = h
+    if mat[0] == "light":
+        return mat[1]
+    s = shade_final(mat, rng, d, rec)
+    if s is None:
+        return (f(0), f(0), f(0))
+    att, sd = s
+    col = ray_color_final(world, tuple(rec[1:4]), sd, time, background, depth - 1, rng, count)
+    return K.add((att[0] * col[0], att[1] * col[1], att[2] * col[2]), (f(0), f(0), f(0)))
+
+
+@pytest.mark.parametrize("x,y", [(20, 12), (12, 25), (28, 20), (6, 8), (3, 15), (18, 18), (33, 12), (9, 36), (24, 15)])
+def test_final_path_equals_oracle_bit_for_bit(x, y, earth):
+    """Pixels of Final at 40 x 40, 4 spp: the ground's Cuboids, the light, a moving sphere, glass, metal, the blue
+    medium inside its glass sphere and the fog (ConstantMedium: two boundary hits, the logarithm of the keyed draw),
+    the Earth (image texture through the sphere's u, v), the Perlin sphere (turbulence) and the 1000 spheres in a
+    rotated, translated BvhNode (pixels chosen so that primary rays hit each of them): colours and world.hit counts
+    equal the oracle's exactly."""
+    W, H, spp, depth, seed = 40, 40, 4, 50, 7
+    info = hrt.preset("final", 1, earth).info
+    world = final_world(np.ascontiguousarray(earth, np.uint8))
+    cam = K.camera(K.F3(info.look_from), K.F3(info.look_at), f(info.fov), f(info.aperture), f(info.focus_dist), W, H)
+    bg = K.F3(info.background)
+    count = [0]
+    total = (f(0), f(0), f(0))
+    for s in range(spp):
+        PATH[0], PATH[1] = K.path_key(seed, y * W + x, s), 0
+        rng = K.Rng(PATH[0])
+        u = (f(x) + rng.gen_f32()) / (f(W) - f(1))
+        v = (f(y) + rng.gen_f32()) / (f(H) - f(1))
+        r = K.camera_ray(cam, u, v, random_in_unit_disk(rng), rng.gen_range(float(info.time0), float(info.time1)))
+        total = K.add(total, ray_color_final(world, tuple(r[0:3]), tuple(r[3:6]), r[6], bg, depth, rng, count))
+    got = tuple(np.sqrt(c * (f(1) / f(spp))) for c in total)
+    ref, cnt = O.OracleScene(hrt.PRESETS["final"], 1, earth).render(W, H, spp, depth, seed=seed, region=(x, y, 1, 1),
+                                                                    threads=1)
+    assert count[0] == cnt["segments"], (count[0], cnt["segments"])
+    for c in range(3):
+        assert np.float32(got[c]).view(np.uint32) == np.float32(ref[0, 0, c]).view(np.uint32), (c, got, ref[0, 0, :3])
