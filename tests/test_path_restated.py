@@ -286,7 +286,7 @@ class Bvh2:
         return right if right is not None else left
 
 
-def cornell_world():
+def cornell_world(smoke=False):
     red, white, green = ("lambertian", SB.v3(0.65, 0.05, 0.05)), ("lambertian", SB.v3(0.73, 0.73, 0.73)), \
         ("lambertian", SB.v3(0.12, 0.45, 0.15))
     light = ("light", SB.v3(15, 15, 15))
@@ -296,7 +296,11 @@ def cornell_world():
             Rect(F(2, 0, 555, 0, 555, 555), white), Rect(F(0, 0, 555, 0, 555, 555), white)]
     for size, angle, off in ((SB.v3(165, 330, 165), 15.0, SB.v3(265, 0, 295)), (SB.v3(165, 165, 165), -18.0, SB.v3(130, 0, 65))):
         sides = HList([Rect(tuple(f(v) for v in r), white) for r in SB.cuboid_rects(SB.v3(0, 0, 0), size)])
-        objs.append(Translate(Rotate(1, sides, angle, (SB.v3(0, 0, 0), size)), off))
+        obj = Translate(Rotate(1, sides, angle, (SB.v3(0, 0, 0), size)), off)
+        if smoke:  # application.rs:723-815: each box a ConstantMedium of density 0.01, black then white smoke
+            n = len(objs) - 6
+            obj = Medium(obj, 0.01, SB.v3(0, 0, 0) if n == 0 else SB.v3(1, 1, 1), n)
+        objs.append(obj)
     return Bvh2(list(range(len(objs))), objs)
 
 
@@ -487,6 +491,33 @@ def test_final_path_equals_oracle_bit_for_bit(x, y, earth):
     got = tuple(np.sqrt(c * (f(1) / f(spp))) for c in total)
     ref, cnt = O.OracleScene(hrt.PRESETS["final"], 1, earth).render(W, H, spp, depth, seed=seed, region=(x, y, 1, 1),
                                                                     threads=1)
+    assert count[0] == cnt["segments"], (count[0], cnt["segments"])
+    for c in range(3):
+        assert np.float32(got[c]).view(np.uint32) == np.float32(ref[0, 0, c]).view(np.uint32), (c, got, ref[0, 0, :3])
+
+
+@pytest.mark.parametrize("x,y", [(20, 10), (12, 14), (28, 16), (8, 30)])
+def test_cornell_smoke_path_equals_oracle_bit_for_bit(x, y):
+    """Cornell-smoke (application.rs:723-815): the two boxes are ConstantMedium boundaries inside Rotation and
+    Translation -- the boundary queried twice through the instance chain, the keyed draw, the Isotropic scatter --
+    the restated path equals the oracle's colours and world.hit counts exactly (40 x 40, 24 spp)."""
+    W, H, spp, depth, seed = 40, 40, 24, 50, 11
+    info = hrt.preset("cornell_smoke", 1).info
+    world = cornell_world(smoke=True)
+    cam = K.camera(K.F3(info.look_from), K.F3(info.look_at), f(info.fov), f(info.aperture), f(info.focus_dist), W, H)
+    bg = K.F3(info.background)
+    count = [0]
+    total = (f(0), f(0), f(0))
+    for s in range(spp):
+        PATH[0], PATH[1] = K.path_key(seed, y * W + x, s), 0
+        rng = K.Rng(PATH[0])
+        u = (f(x) + rng.gen_f32()) / (f(W) - f(1))
+        v = (f(y) + rng.gen_f32()) / (f(H) - f(1))
+        r = K.camera_ray(cam, u, v, random_in_unit_disk(rng), rng.gen_range(float(info.time0), float(info.time1)))
+        total = K.add(total, ray_color_final(world, tuple(r[0:3]), tuple(r[3:6]), r[6], bg, depth, rng, count))
+    got = tuple(np.sqrt(c * (f(1) / f(spp))) for c in total)
+    ref, cnt = O.OracleScene(hrt.PRESETS["cornell_smoke"], 1).render(W, H, spp, depth, seed=seed, region=(x, y, 1, 1),
+                                                                     threads=1)
     assert count[0] == cnt["segments"], (count[0], cnt["segments"])
     for c in range(3):
         assert np.float32(got[c]).view(np.uint32) == np.float32(ref[0, 0, c]).view(np.uint32), (c, got, ref[0, 0, :3])
