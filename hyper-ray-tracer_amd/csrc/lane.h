@@ -204,7 +204,7 @@ struct TRay {
  * executes the core AND the ~11-instruction IEEE sequence and selects (measured cheaper than a
  * branch); HRT_DIV_VOTE 1 puts the fallback behind a wave vote instead.  Only the camera divisions
  * (start_sample) run the bare 3-instruction core, with no fallback. */
-HRT_LANE_FI float div_rn_y(float a) { return a >= 0x1p-49f && a <= 0x1p49f ? 1.0f / a : u2f(0x7fc00000u); }
+HRT_LANE_FI float div_rn_y(float a) { return a >= 0x1p-49f && a <= 0x1p49f ? rcp_fast(a) : u2f(0x7fc00000u); }
 HRT_LANE_FI float div_rn(float x, float a, float y) {
   const float q0 = x * y;
   float q = fmaf(fmaf(-q0, a, x), y, q0);
@@ -242,11 +242,24 @@ HRT_LANE_FI void set_noinv(TRay& r) {
 HRT_LANE_FI bool nan_mode(const TRay& r) { return r.noinv.x != r.noinv.x; }
 
 /* a new origin/direction; the ray keeps its time */
+/* (1/d.x, 1/d.y, 1/d.z) with IEEE division's bits (hd_math.h rcp_fast): one wave vote for the three; the lanes
+ * with a component outside the fast range (a zero, denormal or huge component) divide */
+HRT_LANE_FI Vec3 inv_rn(Vec3 d) {
+  Vec3 q = v3(rcp_fast(d.x), rcp_fast(d.y), rcp_fast(d.z));
+#if defined(__HIP_DEVICE_COMPILE__) && HRT_RCP_FAST
+  const bool ok = (int)rcp_fast_domain(d.x) & (int)rcp_fast_domain(d.y) & (int)rcp_fast_domain(d.z);
+  if (__builtin_amdgcn_ballot_w64(!ok)) {
+    if (!ok) q = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  }
+#endif
+  return q;
+}
+
 HRT_LANE_FI void set_dir(TRay& r, Vec3 o, Vec3 d) {
   r.o = o;
   r.d = d;
   /* aabb.rs:22 computes 1/d per call; the value is the same every time */
-  r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  r.inv = inv_rn(d);
   set_noinv(r);
   r.dd = dot(d, d);
   r.rdd = div_rn_y(r.dd);
@@ -630,7 +643,7 @@ HRT_LANE_FI void inst_enter(const G::Inst& in, TRay& r) {
   if ((in.kind & G::I_KIND_MASK) == G::I_TRANSLATE) return;
   r.d = nd;
   if (in.kind & G::IF_INV) {
-    r.inv = v3(1.0f / nd.x, 1.0f / nd.y, 1.0f / nd.z);
+    r.inv = inv_rn(nd);
     set_noinv(r); /* NaN mode in this frame (box_hit) */
   }
   if (in.kind & G::IF_DD) {
@@ -648,7 +661,7 @@ HRT_LANE_FI void inst_leave(const KParams& P, const G::Inst& in, TRay& r, Vec3 b
   if ((in.kind & G::I_KIND_MASK) == G::I_TRANSLATE) return;
   r.d = nd;
   if (in.kind & G::IF_INV) {
-    r.inv = v3(1.0f / nd.x, 1.0f / nd.y, 1.0f / nd.z);
+    r.inv = inv_rn(nd);
     set_noinv(r); /* NaN mode in this frame (box_hit) */
   }
   if (in.kind & G::IF_DD) {
@@ -1183,7 +1196,7 @@ HRT_LANE_FI bool scatter(PathState& ps, const Rec& rec, uint32_t kind, Vec3 albe
     scattered = dot(ndir, rec.n) > 0.0f;
     att = albedo;
   } else if (kind == G::M_DIELECTRIC) { /* dielectric.rs:31-55 */
-    float ratio = rec.front ? (1.0f / ior) : ior;
+    float ratio = rec.front ? rcp_rn(ior) : ior;
     Vec3 ud = normalize(rd);
     float cos_theta = min_rs(dot(-ud, rec.n), 1.0f);
     float sin_theta = sqrtf(1.0f - cos_theta * cos_theta);
@@ -1584,7 +1597,7 @@ HRT_LANE_FI void chain_turn(const float4 c0, const float4 c1, const float4 c2, c
 HRT_LANE_FI void chain_derived(uint32_t flags, TRay& lr) {
   /* 1/d and d.d of the turned direction where the program reads them (layout.h GL_INV / GL_DD) */
   if (flags & G::GL_INV) {
-    lr.inv = v3(1.0f / lr.d.x, 1.0f / lr.d.y, 1.0f / lr.d.z);
+    lr.inv = inv_rn(lr.d);
     set_noinv(lr); /* NaN mode in the innermost frame (box_hit in the program) */
   }
   if (flags & G::GL_DD) {

@@ -37,6 +37,38 @@ namespace hrt {
  * ----------------------------------------------------------------------------------------------*/
 HRT_HD uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
 HRT_HD float u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+
+/* RN(1 / x), the IEEE quotient 1.0f / x.  On the device, for x whose biased exponent lies in
+ * [RCP_FAST_EXP_LO, RCP_FAST_EXP_HI], v_rcp_f32 followed by one fma Newton step, y + y (1 - x y): 3 instructions
+ * instead of the ~11 of the IEEE division sequence.  That it is the IEEE quotient bit for bit was checked on the
+ * MI355X for EVERY f32 of that range (tests/native/rcp_check.hip, profiles/r06_rcp_check.txt).  rcp_fast: x known
+ * to lie in that range; rcp_rn: any x, the lanes outside the range (0, denormals, huge, inf, NaN) take the IEEE
+ * division under a wave vote.  The host (oracle, lane simulator) divides. */
+#ifndef HRT_RCP_FAST
+#define HRT_RCP_FAST 1
+#endif
+constexpr uint32_t RCP_FAST_EXP_LO = 1u, RCP_FAST_EXP_HI = 252u; /* |x| in [2^-126, 2^126): every such x checked */
+HRT_HD bool rcp_fast_domain(float x) { return ((f2u(x) >> 23) & 255u) - RCP_FAST_EXP_LO <= RCP_FAST_EXP_HI - RCP_FAST_EXP_LO; }
+HRT_HD float rcp_fast(float x) {
+#if defined(__HIP_DEVICE_COMPILE__) && HRT_RCP_FAST
+  const float y = __builtin_amdgcn_rcpf(x);
+  return fmaf(fmaf(-x, y, 1.0f), y, y);
+#else
+  return 1.0f / x;
+#endif
+}
+HRT_HD float rcp_rn(float x) {
+#if defined(__HIP_DEVICE_COMPILE__) && HRT_RCP_FAST
+  float q = rcp_fast(x);
+  const bool ok = rcp_fast_domain(x);
+  if (__builtin_amdgcn_ballot_w64(!ok)) { /* a wave-uniform branch: the IEEE sequence only when a lane needs it */
+    if (!ok) q = 1.0f / x;
+  }
+  return q;
+#else
+  return 1.0f / x;
+#endif
+}
 HRT_HD uint64_t d2u(double d) { uint64_t u; memcpy(&u, &d, 8); return u; }
 HRT_HD double u2d(uint64_t u) { double d; memcpy(&d, &u, 8); return d; }
 
