@@ -1542,6 +1542,9 @@ HRT_LANE_FI void walk_box(const WalkSrc& src, uint32_t& i, const TRay& r, float 
   i = box_ce<FMA, NANG>(a, b, r, tmin, closest) ? f2u(b.w) : skip;
 }
 
+#ifndef HRT_LEAF_HOIST
+#define HRT_LEAF_HOIST 0
+#endif
 /* The parked leaf's primitive: the reference test on its box (aabb.rs, monotone: leaves suffice, DESIGN
  * section 4), then the sphere test against the lane's closest; the walk continues behind the leaf. */
 template <bool COUNT, int WMEM>
@@ -1549,13 +1552,21 @@ HRT_LANE_FI void walk_leaf_test(const KParams& P, const WalkSrc& src, uint32_t l
                                 uint32_t& winner, Counts& cn) {
   constexpr int MEM = payload_mem<WMEM>();
   const float4 bmn = wload<MEM>(src, leaf), bmx = wload<MEM>(src, leaf + 16u);
+  /* a global payload (hybrid and buffer streams): the sphere's parts read with the box, one round trip instead
+   * of up to three dependent ones (box -> centre -> motion; HRT_LEAF_HOIST: 1 the centre, 2 the motion too, which
+   * 80% of the random scenes' spheres have).  Measured no faster on C4's 1/8 share (the other waves hide the
+   * dependent reads; profiles/r06_leaf_hoist_ab.txt), so off by default. */
+  constexpr bool HOIST = HRT_LEAF_HOIST && MEM == WM_BUF;
+  float4 s0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), s1 = s0;
+  if constexpr (HOIST) s0 = wload<MEM>(src, leaf + 32u);
+  if constexpr (HOIST && HRT_LEAF_HOIST > 1) s1 = wload<MEM>(src, leaf + 48u);
   const uint32_t w = f2u(bmn.w);
   if (!(w & G::WL_NOBOX) && !box_ref(bmn, bmx, r, P.t_min, closest)) return;
   if constexpr (COUNT) cn.prims++;
-  const float4 s0 = wload<MEM>(src, leaf + 32u);
+  if constexpr (!HOIST) s0 = wload<MEM>(src, leaf + 32u);
   Vec3 c = v3(s0.x, s0.y, s0.z);
   if (w & G::WL_MOVING) { /* moving_sphere.rs:55-58 */
-    const float4 s1 = wload<MEM>(src, leaf + 48u);
+    if constexpr (!(HOIST && HRT_LEAF_HOIST > 1)) s1 = wload<MEM>(src, leaf + 48u);
     const float f = P.motion_uniform ? r.tau : (r.tau - s0.w) / s1.w; /* r.tau: the time (TRay) */
     c = c + f * v3(s1.x, s1.y, s1.z);
   }
