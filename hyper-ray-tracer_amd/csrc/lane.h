@@ -590,17 +590,48 @@ HRT_LANE_FI bool rect_t(const G::Prim* pp, uint32_t plane, const TRay& r, float 
   return rect_tv(ld4(pp->p0), pp->p1[0], plane, r, tmin, tmax, tout);
 }
 
+/* rotation.rs:104-117 about axis AX (a, b the axes after it): the components picked at compile time */
+template <int AX>
+HRT_LANE_FI void rotate_axis(float s, float c, Vec3& o, Vec3& d) {
+  constexpr int a = (AX + 1) % 3, b = (AX + 2) % 3;
+  const float oa = comp(o, a), ob = comp(o, b), da = comp(d, a), db = comp(d, b);
+  o = with2(o, a, c * oa + s * ob, b, -s * oa + c * ob);
+  d = with2(d, a, c * da + s * db, b, -s * da + c * db);
+}
+/* The same operations for a per-lane axis.  HRT_ROT_SPECIAL 1 (default): a wave whose lanes all turn about y (every
+ * reference scene: RotateY only) runs rotate_axis<1>, its components fixed at compile time, instead of the run-time
+ * axis arithmetic and the component selects of the generic form below; 2: one branch per axis (more registers);
+ * 0: the generic form only.  Same operations on the same operands, so the bits are the same
+ * (tests/test_lane_sim.py::test_rotation_forms_bit_identical).  r06: C5's 1/8 share +7.6%, Final +3.2%
+ * (profiles/r06_rotation_ab.txt). */
+#ifndef HRT_ROT_SPECIAL
+#define HRT_ROT_SPECIAL 1
+#endif
+HRT_LANE_FI void rotate_any(uint32_t axis, float s, float c, Vec3& o, Vec3& d) {
+#if HRT_ROT_SPECIAL == 1 && defined(__HIP_DEVICE_COMPILE__)
+  if (!__builtin_amdgcn_ballot_w64(axis != 1u)) { /* every lane about y */
+    rotate_axis<1>(s, c, o, d);
+    return;
+  }
+#elif HRT_ROT_SPECIAL == 2
+  if (axis == 1u) rotate_axis<1>(s, c, o, d);
+  else if (axis == 0u) rotate_axis<0>(s, c, o, d);
+  else rotate_axis<2>(s, c, o, d);
+  return;
+#endif
+  const int a = (int)(axis + 1) % 3, b = (int)(axis + 2) % 3;
+  const float oa = comp(o, a), ob = comp(o, b), da = comp(d, a), db = comp(d, b);
+  o = with2(o, a, c * oa + s * ob, b, -s * oa + c * ob);
+  d = with2(d, a, c * da + s * db, b, -s * da + c * db);
+}
+
 /* translation.rs:26-30 and rotation.rs:104-117: the ray handed to the child */
 HRT_LANE_FI void inst_ray(const G::Inst& in, Vec3& o, Vec3& d) {
   if ((in.kind & G::I_KIND_MASK) == G::I_TRANSLATE) {
     o = o - v3(in.d[0], in.d[1], in.d[2]);
     return;
   }
-  int a = (int)(in.axis + 1) % 3, b = (int)(in.axis + 2) % 3;
-  float s = in.sin_t, c = in.cos_t;
-  const float oa = comp(o, a), ob = comp(o, b), da = comp(d, a), db = comp(d, b);
-  o = with2(o, a, c * oa + s * ob, b, -s * oa + c * ob);
-  d = with2(d, a, c * da + s * db, b, -s * da + c * db);
+  rotate_any(in.axis, in.sin_t, in.cos_t, o, d);
 }
 
 /* The ray in the frame of instance q's children: the world ray through q's enclosing chain, outermost
@@ -612,12 +643,7 @@ HRT_LANE_FI void chain_level(const float4 v, Vec3& o, Vec3& d) {
     o = o - v3(v.x, v.y, v.z);
     return;
   }
-  const int axis = (int)f2u(v.z);
-  int a = (axis + 1) % 3, b = (axis + 2) % 3;
-  float s = v.x, c = v.y;
-  const float oa = comp(o, a), ob = comp(o, b), da = comp(d, a), db = comp(d, b);
-  o = with2(o, a, c * oa + s * ob, b, -s * oa + c * ob);
-  d = with2(d, a, c * da + s * db, b, -s * da + c * db);
+  rotate_any(f2u(v.z), v.x, v.y, o, d);
 }
 
 /* the first `levels` levels of instance q's chain (all of them: q's children's frame) */
@@ -1643,6 +1669,17 @@ HRT_LANE_FI void gwalk_one(const KParams& P, const G::Node* __restrict__ nodes, 
   if (inst) {
     chain_turn(c0, c1, c2, ch, lr.o, lr.d);
     chain_derived(flags, lr);
+#if HRT_EXP_CHAIN2 && defined(__HIP_DEVICE_COMPILE__) /* timing-only: the turn done twice (its cost, same images) */
+    TRay l2 = r;
+    float z = 0.0f;
+    asm volatile("" : "+v"(z));
+    l2.o.x += z;
+    l2.d.x += z;
+    chain_turn(c0, c1, c2, ch, l2.o, l2.d);
+    chain_derived(flags, l2);
+    asm volatile("" :: "v"(l2.o.x), "v"(l2.o.y), "v"(l2.o.z), "v"(l2.d.x), "v"(l2.d.y), "v"(l2.d.z), "v"(l2.inv.x),
+                 "v"(l2.inv.y), "v"(l2.inv.z), "v"(l2.noinv.x), "v"(l2.noinv.y), "v"(l2.noinv.z), "v"(l2.dd), "v"(l2.rdd));
+#endif
   }
   if constexpr (COUNT) cn.nodes++;
   if (((kp >> 24) & G::KIND_MASK) == G::K_BOX_PRIM &&

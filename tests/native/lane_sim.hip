@@ -236,10 +236,19 @@ void render_pixel(const KParams& P, uint32_t px, uint32_t py, float* rgba, uint6
           WalkSrc src;
           src.base = P.walk;
           src.half = P.walk_half;
+          uint32_t last_chain = G::NONE; /* pricing: instance-chain leaves and repeats of the previous chain */
           while (node < P.walk_end) {
             walk_box<true, WM_HOST>(src, node, r, P.t_min, closest, cn);
-            if (walk_pending(node))
+            if (walk_pending(node)) {
+              const uint32_t leaf = node - G::WALK_PEND;
+              const float4 h = wload<WM_HOST>(src, leaf), bmn = wload<WM_HOST>(src, leaf + 16u);
+              if (f2u(h.z) & G::GL_INST) {
+                cnt[5]++;                                    /* cnt[5]: leaf tests of instance-chain leaves */
+                if (f2u(bmn.w) == last_chain) cnt[6]++;      /* cnt[6]: ... whose chain the previous one shared */
+                last_chain = f2u(bmn.w);
+              }
               gwalk_prim<true, true, WM_HOST>(P, P.nodes, P.prims, src, node, r, closest, winner, gstate, ps.pk, cn);
+            }
           }
           traced = node != G::NONE;
           done = true;
@@ -696,4 +705,21 @@ extern "C" float lane_sim_perlin(const float* ranvec, const uint32_t* perm, int 
   }
   const Vec3 q = v3(p[0], p[1], p[2]);
   return op == 0 ? perlin_noise(&pn, q) : noise_value_t(&pn, scale, q);
+}
+
+/* rotation.rs:104-117 in both of lane.h's forms on the same rays: the run-time-axis form (rotate_any on the host)
+ * and the per-axis instantiation the device runs for a wave turning about one axis (rotate_axis<AX>);
+ * out[12 i ...] = generic o, d, then specialised o, d */
+extern "C" void lane_sim_rotate(uint32_t n, const uint32_t* axis, const float* sc, const float* od, float* out) {
+  for (uint32_t i = 0; i < n; i++) {
+    const float s = sc[2 * i], c = sc[2 * i + 1];
+    Vec3 o = v3(od[6 * i], od[6 * i + 1], od[6 * i + 2]), d = v3(od[6 * i + 3], od[6 * i + 4], od[6 * i + 5]);
+    Vec3 go = o, gd = d;
+    rotate_any(axis[i], s, c, go, gd);
+    if (axis[i] == 0u) rotate_axis<0>(s, c, o, d);
+    else if (axis[i] == 1u) rotate_axis<1>(s, c, o, d);
+    else rotate_axis<2>(s, c, o, d);
+    const float v[12] = {go.x, go.y, go.z, gd.x, gd.y, gd.z, o.x, o.y, o.z, d.x, d.y, d.z};
+    for (int k = 0; k < 12; k++) out[12 * i + k] = v[k];
+  }
 }

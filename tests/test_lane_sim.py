@@ -713,3 +713,21 @@ def test_leaf_skip_is_its_payload_successor(earth, name):
             else:
                 stack += [int(u[pas // 4 + 3]), pas]
         assert leaves > 0
+
+
+def test_rotation_forms_bit_identical(sim):
+    """lane.h rotate_any's run-time-axis form and rotate_axis<AX> (what a wave turning about one axis runs on the
+    device, HRT_ROT_SPECIAL) give the same bits, on ordinary, huge, tiny, zero and signed-zero components."""
+    rng = np.random.default_rng(7)
+    n = 200_000
+    axis = rng.integers(0, 3, n).astype(np.uint32)
+    ang = rng.uniform(-np.pi, np.pi, n)
+    sc = np.stack([np.sin(ang), np.cos(ang)], 1).astype(np.float32)
+    od = (rng.standard_normal((n, 6)) * 10.0 ** rng.integers(-30, 30, (n, 6))).astype(np.float32)
+    od[rng.random((n, 6)) < 0.05] = 0.0
+    od[rng.random((n, 6)) < 0.05] = -0.0
+    out = np.zeros((n, 12), np.float32)
+    vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    sim.lane_sim_rotate(ctypes.c_uint32(n), vp(axis), vp(sc), vp(od), vp(out))
+    assert np.array_equal(out[:, :6].view(np.uint32), out[:, 6:].view(np.uint32))
+    assert not np.array_equal(out[:, :6], od)  # the rays did turn
