@@ -574,7 +574,29 @@ HRT_LANE_FI void plane_axes(uint32_t plane, int& k, int& a, int& b) {
 }
 
 /* rect.rs:53-68 (p0 and k = p1[0] of the record) */
+/* rect.rs:61-70 with the plane's axes fixed at compile time */
+template <int K, int A, int B>
+HRT_LANE_FI bool rect_axes(const float4 p0, float kk, const TRay& r, float tmin, float tmax, float& tout) {
+  float t = (kk - comp(r.o, K)) / comp(r.d, K);
+  if (t < tmin || t > tmax) return false;
+  float av = comp(r.o, A) + t * comp(r.d, A);
+  float bv = comp(r.o, B) + t * comp(r.d, B);
+  if (av < p0.x || av > p0.y || bv < p0.z || bv > p0.w) return false;
+  tout = t;
+  return true;
+}
+#ifndef HRT_RECT_SPECIAL
+#define HRT_RECT_SPECIAL 0 /* 1: a wave whose lanes test rects of one plane runs rect_axes for it (as rotate_any) */
+#endif
 HRT_LANE_FI bool rect_tv(const float4 p0, float kk, uint32_t plane, const TRay& r, float tmin, float tmax, float& tout) {
+#if HRT_RECT_SPECIAL && defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t pw = __builtin_amdgcn_readfirstlane(plane);
+  if (!__builtin_amdgcn_ballot_w64(plane != pw)) {
+    if (pw == HRT_PLANE_XY) return rect_axes<2, 0, 1>(p0, kk, r, tmin, tmax, tout);
+    if (pw == HRT_PLANE_YZ) return rect_axes<0, 1, 2>(p0, kk, r, tmin, tmax, tout);
+    return rect_axes<1, 2, 0>(p0, kk, r, tmin, tmax, tout);
+  }
+#endif
   int k, a, b;
   plane_axes(plane, k, a, b);
   float t = (kk - comp(r.o, k)) / comp(r.d, k);
