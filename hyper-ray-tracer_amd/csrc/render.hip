@@ -263,6 +263,8 @@ __global__ void math_kernel(int op, const float* x, const float* y, float* out, 
     case 5: r = pow5_f(a); break;
     case 6: r = tan_f(a); break;
     case 7: r = div_rn(a, b, div_rn_y(b)); break; /* the walk's division by dot(d, d) */
+    case 8: r = __int_as_float(sat_f2i32(a)); break; /* Rust `as i32` (the Perlin lattice): the bits */
+    case 9: r = __uint_as_float(sat_f2u32(a)); break; /* Rust `as u32` (image texel indices): the bits */
   }
   out[i] = r;
 }
@@ -1232,7 +1234,7 @@ hrt_status hrt_last_launch(hrt_launch_info* out) {
 
 hrt_status hrt_debug_device_math(int32_t op, const float* x, const float* y, float* out, uint32_t n) {
   return hguard([&] {
-    if (!x || !out || op < 0 || op > 7) throw HipError{HRT_ERR_INVALID_ARG, "bad argument"};
+    if (!x || !out || op < 0 || op > 9) throw HipError{HRT_ERR_INVALID_ARG, "bad argument"};
     if (n == 0) return;
     DevBuf<float> x_buf((size_t)n * 4), o_buf((size_t)n * 4), y_buf(y ? (size_t)n * 4 : 4);
     float *dx = x_buf.p, *dy = y ? y_buf.p : nullptr, *dout = o_buf.p;

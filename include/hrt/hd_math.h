@@ -111,17 +111,37 @@ HRT_HD Vec3 refract(Vec3 uv, Vec3 n, float etai_over_etat) {
   return r_out_perp + r_out_parallel;
 }
 
-/* Rust saturating float->int casts (`as i32`, `as u32`) */
+/* Rust saturating float->int casts (`as i32`, `as u32`).  On the device these are the gfx950 conversions
+ * themselves: v_cvt_i32_f32 / v_cvt_u32_f32 truncate toward zero, clamp out-of-range values (infinities
+ * included) to the type's range and turn NaN into 0 -- Rust's saturating semantics, one instruction instead of
+ * the compiler's three nested range branches per conversion (the Perlin lattice indices: 3 per octave, 21 per
+ * noise texture call).  tests/test_gpu_parity.py::test_device_float_to_int_casts holds them to the host's
+ * branchy form bit for bit on every edge value (HRT_HW_CVT=0 keeps the branches on the device, for A/B). */
+#ifndef HRT_HW_CVT
+#define HRT_HW_CVT 1
+#endif
 HRT_HD int32_t sat_f2i32(float f) {
+#if defined(__HIP_DEVICE_COMPILE__) && HRT_HW_CVT
+  int32_t r;
+  asm("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(f));
+  return r;
+#else
   if (!(f == f)) return 0;
   if (f >= 2147483648.0f) return 2147483647;
   if (f < -2147483648.0f) return (int32_t)(-2147483647 - 1);
   return (int32_t)f;
+#endif
 }
 HRT_HD uint32_t sat_f2u32(float f) {
+#if defined(__HIP_DEVICE_COMPILE__) && HRT_HW_CVT
+  uint32_t r;
+  asm("v_cvt_u32_f32 %0, %1" : "=v"(r) : "v"(f));
+  return r;
+#else
   if (!(f == f) || f <= 0.0f) return 0u;
   if (f >= 4294967296.0f) return 4294967295u;
   return (uint32_t)f;
+#endif
 }
 
 /* ------------------------------------------------------------------------------------------------

@@ -388,8 +388,8 @@ hrt_status hrt_debug_poke_blob(hrt_scene* s, uint64_t offset, const void* data, 
 /* The flattened 48-byte record of a primitive (order 0: reference pre-order, 1: SAH streams). */
 hrt_status hrt_debug_prim_record(const hrt_scene* s, int32_t order, uint32_t index, float* out12);
 /* Evaluate the shared deterministic math on the DEVICE (op: 0 sin, 1 cos, 2 acos, 3 atan2, 4 ln,
- * 5 pow5, 6 tan, 7 the walk's division x / y) for n inputs; used by the GPU KAT test to prove
- * host/device bit identity. */
+ * 5 pow5, 6 tan, 7 the walk's division x / y, 8 / 9 the saturating casts `as i32` / `as u32` with the
+ * integer's bits in out) for n inputs; used by the GPU KAT test to prove host/device bit identity. */
 hrt_status hrt_debug_device_math(int32_t op, const float* x, const float* y, float* out, uint32_t n);
 /* The walk's inflated box test (CULL_EXACT's culling half, lane.h box_ce; form 0: sub/mul/add, 1: the fused
  * o*inv form) on every (box, ray) pair, on the DEVICE (on_device = 1: the calling thread's current HIP device) or with the same code compiled for

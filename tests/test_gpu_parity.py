@@ -97,6 +97,38 @@ def test_device_math_bit_identical():
         assert np.array_equal(d.view(np.uint32), h.view(np.uint32)), f"op {op}: {np.sum(d != h)} differ"
 
 
+def _rust_cast(x, signed):
+    """Rust's saturating `x as i32` / `x as u32` (truncation toward zero, NaN -> 0, clamped), in float64."""
+    lo, hi = (-2.0 ** 31, 2.0 ** 31 - 1) if signed else (0.0, 2.0 ** 32 - 1)
+    t = np.trunc(np.nan_to_num(x.astype(np.float64), nan=0.0, posinf=hi, neginf=lo))
+    return np.clip(t, lo, hi).astype(np.int64).astype(np.int32 if signed else np.uint32)
+
+
+@pytest.mark.gpu
+def test_device_float_to_int_casts():
+    """hd_math sat_f2i32 / sat_f2u32 on the device (v_cvt_i32_f32 / v_cvt_u32_f32, HRT_HW_CVT) equal Rust's
+    saturating casts on every edge: NaNs of both signs and payloads, infinities, the limits of the range and
+    their neighbours, signed zeros, values just below and above integers, denormals, and random values of
+    every exponent (the Perlin lattice `floor(p) as i32`, perlin_noise.rs:86-88; the image texel
+    `(u * w) as u32`, image_texture.rs)."""
+    rng = np.random.default_rng(5)
+    edge = np.array([0.0, -0.0, 0.5, -0.5, 0.9999999, -0.9999999, 1.0, -1.0, 1.5, -1.5, 2.5, -2.5, 255.99998,
+                     2.0 ** 31, -2.0 ** 31, 2.0 ** 32, -2.0 ** 32, 3e38, -3e38, np.inf, -np.inf, np.nan, -np.nan,
+                     1e-45, -1e-45, 1.17e-38, 16777217.0, 8388607.5], np.float32)
+    near = np.array([2.0 ** 31, 2.0 ** 32, 2.0 ** 24, 1.0], np.float32)
+    neigh = np.concatenate([np.nextafter(near, np.float32(np.inf)), np.nextafter(near, np.float32(-np.inf))])
+    nans = np.array([0x7fc00000, 0xffc00000, 0x7f800001, 0xff812345, 0x7fffffff], np.uint32).view(np.float32)
+    rand = (rng.uniform(-1, 1, 300000) * 2.0 ** rng.uniform(-30, 40, 300000)).astype(np.float32)
+    bits = rng.integers(0, 2 ** 32, 100000, dtype=np.uint64).astype(np.uint32).view(np.float32)
+    x = np.concatenate([edge, neigh, -neigh, nans, rand, bits])
+    with np.errstate(invalid="ignore"):
+        for op, signed in ((8, True), (9, False)):
+            d = hrt.device_math(op, x).view(np.int32 if signed else np.uint32)
+            want = _rust_cast(x, signed)
+            bad = np.flatnonzero(d != want)
+            assert bad.size == 0, (op, x[bad[:5]], d[bad[:5]], want[bad[:5]])
+
+
 @pytest.mark.gpu
 def test_repeated_calls_on_two_streams(earth):
     """Many back-to-back tile renders on two HIP streams (scratch-slot reuse) all match a single
