@@ -68,6 +68,37 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 template <bool LDS, bool FAST>
 constexpr int block_threads() { return LDS ? (FAST ? 1024 : 512) : 256; }
 
+/* LDS staging of n Perlin tables at dst (an LDS address that is a multiple of PERLIN_LDS_ALIGN; layout.h Perlin).
+ * HRT_PERLIN_XADDR (default): each permutation word v becomes v << 4, its ranvec entry's byte offset in the table
+ * (< 4096), and the x permutation's also carries the table's own LDS address (a multiple of 4096), so the gradient
+ * of a lattice corner is at LDS address px ^ py ^ pz (lane.h perlin_noise_t<true>): the three words XOR to the
+ * address with no shift and add per corner. */
+__device__ __forceinline__ const G::Perlin* stage_perlin(float4* dst, const G::Perlin* src, uint32_t n) {
+  const float4* g = reinterpret_cast<const float4*>(src);
+  constexpr uint32_t PER = (uint32_t)(sizeof(G::Perlin) / 16u), RV = 256u, PW = G::PERM_N / 4u; /* float4s */
+  const uint32_t n4 = n * PER;
+  const uint32_t at = (uint32_t)(size_t)(__attribute__((address_space(3))) float4*)dst;
+  for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) {
+    float4 v = g[k];
+#if HRT_PERLIN_XADDR
+    const uint32_t t = k / PER, w = k - t * PER;
+    if (w >= RV && w < RV + 3u * PW) {
+      const uint32_t base = w < RV + PW ? at + t * (uint32_t)sizeof(G::Perlin) : 0u;
+      v = make_float4(__uint_as_float((__float_as_uint(v.x) << 4) | base), __uint_as_float((__float_as_uint(v.y) << 4) | base),
+                      __uint_as_float((__float_as_uint(v.z) << 4) | base), __uint_as_float((__float_as_uint(v.w) << 4) | base));
+    }
+#endif
+    dst[k] = v;
+  }
+  return reinterpret_cast<const G::Perlin*>(dst);
+}
+
+/* the LDS float4 at or after p whose address is a multiple of a (dynamic LDS) */
+__device__ __forceinline__ float4* lds_align(float4* p, uint32_t a) {
+  const uint32_t at = (uint32_t)(size_t)(__attribute__((address_space(3))) float4*)p;
+  return p + (((at + a - 1u) & ~(a - 1u)) - at) / 16u;
+}
+
 /* Copy the node stream and primitive records into this workgroup's LDS.  BYTE_LINKS: store each skip
  * link as the LDS byte address of its target (base + skip x sizeof(Node)), for walks whose position is
  * that address (basic_box STRIDE 32). */

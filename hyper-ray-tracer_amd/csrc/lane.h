@@ -1003,7 +1003,12 @@ HRT_LANE Rec make_record(const KParams& P, uint32_t winner, float t, Vec3 wo, Ve
 #ifndef HRT_PERLIN_SELECT
 #define HRT_PERLIN_SELECT 1 /* r06: C3 +1.3% (17 218 -> 17 445 Mrays/s, profiles/r06_perlin_select_ab.txt) */
 #endif
-template <class PN>
+#ifndef HRT_PERLIN_XADDR
+#define HRT_PERLIN_XADDR 1 /* tables staged in LDS carry their gradients' addresses (kernel_common.h stage_perlin) */
+#endif
+/* XADDR: `pn` is an LDS pointer to tables staged by stage_perlin, whose permutation words XOR to the gradient's LDS
+ * address; otherwise the layout.h tables as built (global memory, the host) */
+template <bool XADDR = false, class PN>
 HRT_LANE_FI float perlin_noise_t(PN pn, Vec3 point) {
   int32_t i = sat_f2i32(floorf(point.x));
   int32_t j = sat_f2i32(floorf(point.y));
@@ -1027,11 +1032,22 @@ HRT_LANE_FI float perlin_noise_t(PN pn, Vec3 point) {
     const int x = idx / 4, y = (idx / 2) % 2, z = idx % 2;
     /* perlin_noise.rs:92-94 `(i + i_x) & 255` in i32, which wraps in a release build at i = i32::MAX (a
      * saturated huge coordinate): the same bits in u32, without C++'s signed-overflow UB (UBSan, r05) */
-    uint32_t px = pn->perm[0][((uint32_t)i + (uint32_t)x) & 255u];
-    uint32_t py = pn->perm[1][((uint32_t)j + (uint32_t)y) & 255u];
-    uint32_t pz = pn->perm[2][((uint32_t)k + (uint32_t)z) & 255u];
-    const uint32_t g_i = px ^ py ^ pz;
-    const Vec3 g = v3(pn->ranvec[g_i][0], pn->ranvec[g_i][1], pn->ranvec[g_i][2]);
+    /* ((i + x) & 255) = (i & 255) + x in the doubled tables (layout.h Perlin) */
+    uint32_t px = pn->perm[0][((uint32_t)i & 255u) + (uint32_t)x];
+    uint32_t py = pn->perm[1][((uint32_t)j & 255u) + (uint32_t)y];
+    uint32_t pz = pn->perm[2][((uint32_t)k & 255u) + (uint32_t)z];
+    Vec3 g;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (XADDR) { /* perlin_noise.rs:96: ranvec[perm_x ^ perm_y ^ perm_z], the XOR already an address */
+      typedef __attribute__((address_space(3))) const float4 lds_f4; /* a 16-B record: one ds_read */
+      const float4 q = *(const lds_f4*)(size_t)(px ^ py ^ pz);
+      g = v3(q.x, q.y, q.z);
+    } else
+#endif
+    {
+      const uint32_t g_i = px ^ py ^ pz;
+      g = v3(pn->ranvec[g_i][0], pn->ranvec[g_i][1], pn->ranvec[g_i][2]);
+    }
     Vec3 weight = v3(u - (float)x, v - (float)y, w - (float)z);
 #if HRT_PERLIN_SELECT
     acc += ((x ? u : u0) * (y ? v : v0)) * (z ? w : w0) * dot(g, weight);
@@ -1045,13 +1061,13 @@ HRT_LANE_FI float perlin_noise_t(PN pn, Vec3 point) {
 HRT_LANE float perlin_noise(const G::Perlin* pn, Vec3 point) { return perlin_noise_t(pn, point); }
 
 /* noise_texture.rs:24-31 + turbulence perlin_noise.rs:66-78 (the scalar part of the texture value) */
-template <class PN>
+template <bool XADDR = false, class PN>
 HRT_LANE_FI float noise_value_t(PN pn, float scale, Vec3 p) {
   Vec3 q = scale * p;
   float accumulator = 0.0f, weight = 1.0f;
 #pragma unroll 1
   for (int o = 0; o < 7; o++) { /* rolled: keeps the code (and the callers' register demand) small */
-    accumulator += weight * perlin_noise_t(pn, q);
+    accumulator += weight * perlin_noise_t<XADDR>(pn, q);
     weight *= 0.5f;
     q = q * 2.0f;
   }
@@ -1066,7 +1082,7 @@ HRT_LANE_NI float noise_value(const G::Perlin* pn, float scale, Vec3 p) {
 #if defined(__HIP_DEVICE_COMPILE__)
   if constexpr (PLDS) {
     typedef __attribute__((address_space(3))) const G::Perlin lds_perlin;
-    return noise_value_t((const lds_perlin*)(size_t)(uint32_t)(size_t)pn, scale, p);
+    return noise_value_t<HRT_PERLIN_XADDR != 0>((const lds_perlin*)(size_t)(uint32_t)(size_t)pn, scale, p);
   }
 #endif
   return noise_value_t(pn, scale, p);
@@ -1140,7 +1156,7 @@ HRT_LANE Vec3 tex_value(const KParams& P, uint32_t id, float u, float v, Vec3 p,
         if constexpr (INL) {
 #if defined(__HIP_DEVICE_COMPILE__)
           typedef __attribute__((address_space(3))) const G::Perlin lds_perlin;
-          if (P.perlin_lds) s = noise_value_t((const lds_perlin*)(size_t)(uint32_t)(size_t)pn, T.a[0], p);
+          if (P.perlin_lds) s = noise_value_t<HRT_PERLIN_XADDR != 0>((const lds_perlin*)(size_t)(uint32_t)(size_t)pn, T.a[0], p);
           else
 #endif
             s = noise_value_t(pn, T.a[0], p);

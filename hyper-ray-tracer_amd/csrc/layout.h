@@ -113,10 +113,19 @@ struct alignas(16) Tex {
   uint32_t i3, pad0, pad1, pad2;
 };
 
+/* perm: each axis's permutation twice over (perm[c][256 + i] = perm[c][i]), so perlin_noise.rs:92-94's
+ * `(i + di) & 255` for di in {0, 1} is the index (i & 255) + di: the second lattice corner's entry is the next word,
+ * one LDS / global read with an immediate offset and no add / mask of its own */
+constexpr uint32_t PERM_N = 512;
+/* 12 KB, three 4-KB pages: the kernels stage the tables in LDS at 4096-aligned addresses (kernel_common.h
+ * stage_perlin), where each permutation word becomes its ranvec entry's address (lane.h perlin_noise_t XADDR) */
+constexpr uint32_t PERLIN_LDS_ALIGN = 4096;
 struct alignas(16) Perlin {
   float ranvec[256][4];
-  uint32_t perm[3][256];
+  uint32_t perm[3][PERM_N];
+  uint32_t pad[512];
 };
+static_assert(sizeof(Perlin) == 3 * PERLIN_LDS_ALIGN, "Perlin tables stage at 4-KB-aligned LDS addresses");
 
 /* tile list entry (device) */
 struct alignas(16) TileDev {

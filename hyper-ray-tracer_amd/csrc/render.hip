@@ -436,8 +436,9 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
     pl.lds = (flags & HRT_RENDER_NO_LDS) == 0 && pl.smem <= LDS_SCENE_MAX;
     const size_t perlin = s->perlin.size() * sizeof(G::Perlin);
     const char* pe = knob_env("HRT_PERLIN_LDS"); /* A/B knob: "0" keeps the Perlin tables in global memory */
-    pl.perlin_lds = pl.lds && perlin > 0 && pl.smem + perlin <= LDS_SCENE_MAX && !(pe && strcmp(pe, "0") == 0);
-    if (pl.perlin_lds) pl.smem += perlin;
+    const size_t at = (pl.smem + G::PERLIN_LDS_ALIGN - 1) / G::PERLIN_LDS_ALIGN * G::PERLIN_LDS_ALIGN; /* stage_perlin */
+    pl.perlin_lds = pl.lds && perlin > 0 && at + perlin <= LDS_SCENE_MAX && !(pe && strcmp(pe, "0") == 0);
+    if (pl.perlin_lds) pl.smem = at + perlin;
   }
   /* the sphere kernel's packet walk (render_sphere.hip PACKET) for streams of at most SPHERE_PACKET_NODES node parts */
   {
@@ -473,8 +474,9 @@ Plan plan(const hrt_scene* s, const hrt_camera* cam, uint32_t flags) {
     pl.smem = pl.gwalk_mem == WM_BUF ? 0 : walk + (pl.gwalk_lref ? ref : 0);
     const size_t perlin = s->perlin.size() * sizeof(G::Perlin);
     const char* pe = knob_env("HRT_PERLIN_LDS");
-    pl.perlin_lds = pl.gwalk_lref && perlin > 0 && pl.smem + perlin <= LDS_SCENE_MAX && !(pe && strcmp(pe, "0") == 0);
-    if (pl.perlin_lds) pl.smem += perlin;
+    const size_t at = (pl.smem + G::PERLIN_LDS_ALIGN - 1) / G::PERLIN_LDS_ALIGN * G::PERLIN_LDS_ALIGN; /* stage_perlin */
+    pl.perlin_lds = pl.gwalk_lref && perlin > 0 && at + perlin <= LDS_SCENE_MAX && !(pe && strcmp(pe, "0") == 0);
+    if (pl.perlin_lds) pl.smem = at + perlin;
     pl.lds = pl.gwalk_mem != WM_BUF;
     /* the packet walk (render_general.hip) for streams of at most GWALK_PACKET_NODES node parts staged whole in
      * LDS with their reference arrays whose leaves run generic programs (s->w_generic: Cornell-smoke's media in

@@ -92,7 +92,7 @@ void render_gwalk_kernel(KParams P) {
     Q.mats = static_cast<const G::Mat*>(stage(P.mats, P.n_mats, sizeof(G::Mat)));
     Q.texs = static_cast<const G::Tex*>(stage(P.texs, P.n_texs, sizeof(G::Tex)));
     Q.chains = static_cast<const float4*>(stage(P.chains, P.n_insts, G::CHAIN_F4 * 16u));
-    if (P.perlin_lds) Q.perlin = static_cast<const G::Perlin*>(stage(P.perlin, P.n_perlin, sizeof(G::Perlin)));
+    if (P.perlin_lds) Q.perlin = stage_perlin(lds_align(dst, G::PERLIN_LDS_ALIGN), P.perlin, P.n_perlin); /* render.hip plan */
     nodes = Q.nodes;
     prims = Q.prims;
   }

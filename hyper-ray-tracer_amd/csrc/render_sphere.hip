@@ -63,13 +63,8 @@ void render_basic_kernel(KParams P) {
     const uint32_t staged = HYB ? P.walk_hot : P.walk_bytes;
     for (uint32_t k = threadIdx.x; k < staged / 16u; k += blockDim.x) lds_scene[k] = g[k];
     if constexpr (HEAVY) {
-      if (P.perlin_lds) {
-        const float4* gp = reinterpret_cast<const float4*>(P.perlin);
-        float4* dst = lds_scene + staged / 16u;
-        const uint32_t n4 = P.n_perlin * (uint32_t)(sizeof(G::Perlin) / 16);
-        for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) dst[k] = gp[k];
-        Q.perlin = reinterpret_cast<const G::Perlin*>(dst);
-      }
+      if (P.perlin_lds) /* at the next 4-KB boundary (render.hip plan sizes the LDS so) */
+        Q.perlin = stage_perlin(lds_align(lds_scene + staged / 16u, G::PERLIN_LDS_ALIGN), P.perlin, P.n_perlin);
     }
     __syncthreads();
     if (lds_base != 0u) { /* no static LDS in this kernel, so this cannot happen: report, do nothing */

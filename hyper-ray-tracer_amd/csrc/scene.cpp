@@ -1951,7 +1951,7 @@ hrt_status hrt_tex_noise(hrt_scene* s, float scale, const float* ranvec, const u
       for (int c = 0; c < 3; c++) p.ranvec[i][c] = ranvec[3 * i + c];
       for (int c = 0; c < 3; c++) {
         need(perm[256 * c + i] < 256, HRT_ERR_INVALID_ARG, "permutation entry >= 256");
-        p.perm[c][i] = perm[256 * c + i];
+        p.perm[c][i] = p.perm[c][256 + i] = perm[256 * c + i]; /* twice over (layout.h Perlin) */
       }
     }
     s->perlin.push_back(p);

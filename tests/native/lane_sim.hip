@@ -701,7 +701,7 @@ extern "C" float lane_sim_perlin(const float* ranvec, const uint32_t* perm, int 
     pn.ranvec[i][1] = ranvec[3 * i + 1];
     pn.ranvec[i][2] = ranvec[3 * i + 2];
     pn.ranvec[i][3] = 0.0f;
-    for (int c = 0; c < 3; c++) pn.perm[c][i] = perm[256 * c + i];
+    for (int c = 0; c < 3; c++) pn.perm[c][i] = pn.perm[c][256 + i] = perm[256 * c + i];
   }
   const Vec3 q = v3(p[0], p[1], p[2]);
   return op == 0 ? perlin_noise(&pn, q) : noise_value_t(&pn, scale, q);

@@ -276,12 +276,14 @@ def test_final_scene_draws_and_structure_restated_independently():
     assert len(inst) == 1000
     for k, o in zip(inst, spheres):
         assert all(_same(prims[k][j], o[1][j]) for j in range(3)) and _same(prims[k][3], 10.0), (k, prims[k][:4])
-    # the noise texture's Perlin tables (layout.h Perlin: ranvec[256][4] f32, then perm[3][256] u32)
-    pt = b[info.off_perlin:info.off_perlin + 7168]
+    # the noise texture's Perlin tables (layout.h Perlin: ranvec[256][4] f32, then perm[3][512] u32: each
+    # permutation twice over)
+    pt = b[info.off_perlin:info.off_perlin + 4096 + 3 * 512 * 4]
     rv = pt[:4096].view(np.float32).reshape(256, 4)
-    pm = pt[4096:].view(np.uint32).reshape(3, 256)
+    pm = pt[4096:].view(np.uint32).reshape(3, 512)
     assert all(_same(rv[i][j], ranvec[i][j]) for i in range(256) for j in range(3))
-    assert [list(map(int, pm[c])) for c in range(3)] == perms
+    assert [list(map(int, pm[c, :256])) for c in range(3)] == perms
+    assert [list(map(int, pm[c, 256:])) for c in range(3)] == perms
 
 
 # ------------------------------------------------------------------------------- application.rs:639-721 (Cornell)
@@ -366,11 +368,12 @@ def test_noise_scenes_restated_independently(name):
     pu = prims.view(np.uint32)
     ranvec, perms = K.perlin_tables(K.scene_rng(1))
     b = np.frombuffer(hrt.scene_blob(hrt.preset(name, 1))[0].raw, np.uint8)
-    pt = b[info.off_perlin:info.off_perlin + 7168]
+    pt = b[info.off_perlin:info.off_perlin + 4096 + 3 * 512 * 4]
     rv = pt[:4096].view(np.float32).reshape(256, 4)
-    pm = pt[4096:].view(np.uint32).reshape(3, 256)
+    pm = pt[4096:].view(np.uint32).reshape(3, 512)  # each permutation twice over (layout.h Perlin)
     assert all(_same(rv[i][j], ranvec[i][j]) for i in range(256) for j in range(3))
-    assert [list(map(int, pm[c])) for c in range(3)] == perms
+    assert [list(map(int, pm[c, :256])) for c in range(3)] == perms
+    assert [list(map(int, pm[c, 256:])) for c in range(3)] == perms
     objs = [("sphere", v3(0, -1000, 0), None, f(1000), "noise"),
             ("sphere", v3(0, 2, 0), None, f(2), "image" if name == "earth_perlin" else "noise")]
     spheres = [p for p in range(len(prims)) if (pu[p, 11] & 3) == 0]
