@@ -87,7 +87,7 @@ struct KParams {
   uint32_t walk_hot;   /* WM_HYB: offsets below this are staged in LDS (layout.h placement) */
   uint32_t lane_lds;   /* sphere kernel: LDS byte offset of the per-lane result slots (after the staged scene) */
   uint32_t n_insts, n_media, n_mats, n_texs; /* record counts (render_gwalk_kernel stages them in LDS) */
-  uint32_t n_perlin;   /* Perlin tables (7 KB each); perlin_lds: the kernel stages them in LDS */
+  uint32_t n_perlin;   /* Perlin tables (12 KB each); perlin_lds: the kernel stages them in LDS (stage_perlin) */
   uint32_t perlin_lds;
   uint32_t walk_half;  /* the walk stream's node-part split (layout.h WALK_SPLIT_HALF) or 16 */
   uint32_t walk_c16;   /* 16-B node parts (layout.h WALK_C16): walk_end is then the node count */
