@@ -1008,11 +1008,16 @@ HRT_LANE Rec make_record(const KParams& P, uint32_t winner, float t, Vec3 wo, Ve
 #endif
 /* XADDR: `pn` is an LDS pointer to tables staged by stage_perlin, whose permutation words XOR to the gradient's LDS
  * address; otherwise the layout.h tables as built (global memory, the host) */
-template <bool XADDR = false, class PN>
+/* HWCVT: the lattice's `floor() as i32` by the hardware conversion (hd_math.h sat_f2i32); otherwise the compare form
+ * (sat_f2i32_cmp).  Only the sphere kernel's HEAVY shading takes it (C3 +4.6-6.4%): in the general kernel the
+ * straight-line octave loop's longer live ranges cost Final 16 B more spills per lane and 3.5 GB of scratch writes per
+ * frame for no time (profiles/r06i_final_summary.md against r06h's) */
+template <bool XADDR = false, bool HWCVT = false, class PN>
 HRT_LANE_FI float perlin_noise_t(PN pn, Vec3 point) {
-  int32_t i = sat_f2i32(floorf(point.x));
-  int32_t j = sat_f2i32(floorf(point.y));
-  int32_t k = sat_f2i32(floorf(point.z));
+  /* perlin_noise.rs:86-88 `floor() as i32` */
+  const int32_t i = HWCVT ? sat_f2i32(floorf(point.x)) : sat_f2i32_cmp(floorf(point.x));
+  const int32_t j = HWCVT ? sat_f2i32(floorf(point.y)) : sat_f2i32_cmp(floorf(point.y));
+  const int32_t k = HWCVT ? sat_f2i32(floorf(point.z)) : sat_f2i32_cmp(floorf(point.z));
   float u = point.x - floorf(point.x);
   float v = point.y - floorf(point.y);
   float w = point.z - floorf(point.z);
@@ -1032,10 +1037,15 @@ HRT_LANE_FI float perlin_noise_t(PN pn, Vec3 point) {
     const int x = idx / 4, y = (idx / 2) % 2, z = idx % 2;
     /* perlin_noise.rs:92-94 `(i + i_x) & 255` in i32, which wraps in a release build at i = i32::MAX (a
      * saturated huge coordinate): the same bits in u32, without C++'s signed-overflow UB (UBSan, r05) */
-    /* ((i + x) & 255) = (i & 255) + x in the doubled tables (layout.h Perlin) */
-    uint32_t px = pn->perm[0][((uint32_t)i & 255u) + (uint32_t)x];
-    uint32_t py = pn->perm[1][((uint32_t)j & 255u) + (uint32_t)y];
-    uint32_t pz = pn->perm[2][((uint32_t)k & 255u) + (uint32_t)z];
+    /* XADDR (LDS): ((i + x) & 255) = (i & 255) + x in the doubled tables (layout.h Perlin), the corner pair one
+     * ds_read2; the global-memory form keeps the masked index into the first copy (the pair as two global loads
+     * cost Final's general kernel 16 B more spills per lane in the out-of-line noise call's saves) */
+    const uint32_t ix = XADDR ? ((uint32_t)i & 255u) + (uint32_t)x : ((uint32_t)i + (uint32_t)x) & 255u;
+    const uint32_t iy = XADDR ? ((uint32_t)j & 255u) + (uint32_t)y : ((uint32_t)j + (uint32_t)y) & 255u;
+    const uint32_t iz = XADDR ? ((uint32_t)k & 255u) + (uint32_t)z : ((uint32_t)k + (uint32_t)z) & 255u;
+    uint32_t px = pn->perm[0][ix];
+    uint32_t py = pn->perm[1][iy];
+    uint32_t pz = pn->perm[2][iz];
     Vec3 g;
 #if defined(__HIP_DEVICE_COMPILE__)
     if constexpr (XADDR) { /* perlin_noise.rs:96: ranvec[perm_x ^ perm_y ^ perm_z], the XOR already an address */
@@ -1061,13 +1071,13 @@ HRT_LANE_FI float perlin_noise_t(PN pn, Vec3 point) {
 HRT_LANE float perlin_noise(const G::Perlin* pn, Vec3 point) { return perlin_noise_t(pn, point); }
 
 /* noise_texture.rs:24-31 + turbulence perlin_noise.rs:66-78 (the scalar part of the texture value) */
-template <bool XADDR = false, class PN>
+template <bool XADDR = false, bool HWCVT = false, class PN>
 HRT_LANE_FI float noise_value_t(PN pn, float scale, Vec3 p) {
   Vec3 q = scale * p;
   float accumulator = 0.0f, weight = 1.0f;
 #pragma unroll 1
   for (int o = 0; o < 7; o++) { /* rolled: keeps the code (and the callers' register demand) small */
-    accumulator += weight * perlin_noise_t<XADDR>(pn, q);
+    accumulator += weight * perlin_noise_t<XADDR, HWCVT>(pn, q);
     weight *= 0.5f;
     q = q * 2.0f;
   }
@@ -1077,15 +1087,15 @@ HRT_LANE_FI float noise_value_t(PN pn, float scale, Vec3 p) {
 /* The noise texture's value with its tables at `pn`.  PLDS (device): the tables are in LDS (`pn` a generic
  * pointer into the kernel's staged tables: its low 32 bits are the LDS address).  Out of line, with every
  * input passed by value (no caller struct through memory). */
-template <bool PLDS>
+template <bool PLDS, bool HWCVT = false>
 HRT_LANE_NI float noise_value(const G::Perlin* pn, float scale, Vec3 p) {
 #if defined(__HIP_DEVICE_COMPILE__)
   if constexpr (PLDS) {
     typedef __attribute__((address_space(3))) const G::Perlin lds_perlin;
-    return noise_value_t<HRT_PERLIN_XADDR != 0>((const lds_perlin*)(size_t)(uint32_t)(size_t)pn, scale, p);
+    return noise_value_t<HRT_PERLIN_XADDR != 0, HWCVT>((const lds_perlin*)(size_t)(uint32_t)(size_t)pn, scale, p);
   }
 #endif
-  return noise_value_t(pn, scale, p);
+  return noise_value_t<false, HWCVT>(pn, scale, p);
 }
 
 /* image_texture.rs:36-62 */
@@ -1139,7 +1149,7 @@ HRT_LANE_FI bool checker_odd(float vx, float vy, float vz) {
 
 /* INL: the noise texture's turbulence inline (a kernel with the registers to spare: a call saves and
  * restores the caller's live registers through scratch) instead of the out-of-line noise_value */
-template <bool FULL, bool COUNT, bool INL = false>
+template <bool FULL, bool COUNT, bool INL = false, bool HWCVT = false>
 HRT_LANE Vec3 tex_value(const KParams& P, uint32_t id, float u, float v, Vec3 p, Counts& cn) {
   for (int guard = 0; guard < 64; guard++) {
     const G::Tex& T = P.texs[id];
@@ -1156,12 +1166,12 @@ HRT_LANE Vec3 tex_value(const KParams& P, uint32_t id, float u, float v, Vec3 p,
         if constexpr (INL) {
 #if defined(__HIP_DEVICE_COMPILE__)
           typedef __attribute__((address_space(3))) const G::Perlin lds_perlin;
-          if (P.perlin_lds) s = noise_value_t<HRT_PERLIN_XADDR != 0>((const lds_perlin*)(size_t)(uint32_t)(size_t)pn, T.a[0], p);
+          if (P.perlin_lds) s = noise_value_t<HRT_PERLIN_XADDR != 0, HWCVT>((const lds_perlin*)(size_t)(uint32_t)(size_t)pn, T.a[0], p);
           else
 #endif
             s = noise_value_t(pn, T.a[0], p);
         } else {
-          s = P.perlin_lds ? noise_value<true>(pn, T.a[0], p) : noise_value<false>(pn, T.a[0], p);
+          s = P.perlin_lds ? noise_value<true, HWCVT>(pn, T.a[0], p) : noise_value<false>(pn, T.a[0], p);
         }
         return (v3(1.0f, 1.0f, 1.0f) * 0.5f) * s;
       }
@@ -1365,7 +1375,7 @@ HRT_LANE_FI bool shade_walk(const KParams& P, const WalkSrc& src, PathState& ps,
     if constexpr (HEAVY) { /* sphere.rs:31-35 (u, v) only under an image texture (Mat.needs_uv) */
       const G::Mat& M = P.mats[rec.mat];
       if (M.needs_uv) sphere_uv(outward, rec.u, rec.v);
-      return tex_value<true, COUNT, HRT_HEAVY_INLINE != 0>(P, M.tex, rec.u, rec.v, rec.p, cn);
+      return tex_value<true, COUNT, HRT_HEAVY_INLINE != 0, true>(P, M.tex, rec.u, rec.v, rec.p, cn); /* HWCVT */
     }
     return tex_value<false, COUNT>(P, P.mats[rec.mat].tex, rec.u, rec.v, rec.p, cn);
   });

@@ -116,20 +116,25 @@ HRT_HD Vec3 refract(Vec3 uv, Vec3 n, float etai_over_etat) {
  * included) to the type's range and turn NaN into 0 -- Rust's saturating semantics, one instruction instead of
  * the compiler's three nested range branches per conversion (the Perlin lattice indices: 3 per octave, 21 per
  * noise texture call).  tests/test_gpu_parity.py::test_device_float_to_int_casts holds them to the host's
- * branchy form bit for bit on every edge value (HRT_HW_CVT=0 keeps the branches on the device, for A/B). */
+ * branchy form bit for bit on every edge value (HRT_HW_CVT=0 keeps the branches on the device, for A/B).
+ * sat_f2i32_cmp: the compare-and-select form everywhere (lane.h: the Perlin lattice over tables in global memory, where
+ * the straight-line octave loop's longer live ranges cost Final's kernel 16 B more spills per lane). */
 #ifndef HRT_HW_CVT
 #define HRT_HW_CVT 1
 #endif
+HRT_HD int32_t sat_f2i32_cmp(float f) {
+  if (!(f == f)) return 0;
+  if (f >= 2147483648.0f) return 2147483647;
+  if (f < -2147483648.0f) return (int32_t)(-2147483647 - 1);
+  return (int32_t)f;
+}
 HRT_HD int32_t sat_f2i32(float f) {
 #if defined(__HIP_DEVICE_COMPILE__) && HRT_HW_CVT
   int32_t r;
   asm("v_cvt_i32_f32 %0, %1" : "=v"(r) : "v"(f));
   return r;
 #else
-  if (!(f == f)) return 0;
-  if (f >= 2147483648.0f) return 2147483647;
-  if (f < -2147483648.0f) return (int32_t)(-2147483647 - 1);
-  return (int32_t)f;
+  return sat_f2i32_cmp(f);
 #endif
 }
 HRT_HD uint32_t sat_f2u32(float f) {
